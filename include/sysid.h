@@ -1,0 +1,135 @@
+/*
+ * sysid.h — C ABI of the MI355X identification-regressor engine (libsysid.so, gfx950).
+ *
+ * Hot path replaced (reference @ xiaohu97/system_identification):
+ *   per sample i:  Y_proj_i = P_i · Y(q_i, dq_i, ddq_i)           src/sys_identification.py:401-410
+ *                  tau_proj_i = P_i · Sᵀ · tau_i                  src/sys_identification.py:409
+ *                  B_v_i = P_i Sᵀ diag(dq_i[6:]), B_c_i = P_i Sᵀ diag(sign(dq_i[6:]))
+ *                                                                  src/sys_identification.py:412-418
+ *                  P_i = I − pinv(J_c,i) J_c,i                     src/sys_identification.py:119-135
+ *   stacked over samples (row block i = rows [i·nv, (i+1)·nv))     demo/spot_identification.py:37-56, 84-87
+ *   plus the normal equations the Solver objective implies        src/solver.py:186-190
+ *        G = Aᵀ A, g = Aᵀ b, bᵀ b  with A = [Y_proj | B_v | B_c], b = tau_proj.
+ *
+ * The reference has no FFI layer; its boundary is the Python method surface.  The Python package
+ * system_identification_amd (ctypes, engine.py) binds exactly these entry points.
+ *
+ * Conventions
+ *   - Inputs are float64, channel-major ("SoA", the reference's .dat layout: one channel per row,
+ *     one sample per column, demo/spot_identification.py:10-14) with leading dimension ld >= N.
+ *   - Contact values: a foot is in contact when its value is non-zero (CONTACT_LOST = 2 counts, as in
+ *     the reference's truthiness test, src/sys_identification.py:125).  Host entry points reject a
+ *     sample whose int(sum(cnt)) is smaller than its number of non-zero feet (the reference raises a
+ *     numpy broadcast error there) with SYSID_E_CONTACT.
+ *   - Return codes: 0 = OK, < 0 = error; nothing is thrown across the ABI.  sysid_last_error() gives
+ *     a message.  Python maps E_INVALID/E_MODEL/E_CONTACT to ValueError, E_DEVICE/E_NOMEM to RuntimeError.
+ *   - A handle is bound to one device and owns one HIP stream; it is not re-entrant across threads.
+ *
+ * Packed model (produced by system_identification_amd.model.Model.pack()), little endian:
+ *   int32  header[16] = {0x44495953 'SYID', version 1, nq, nv, njoints, n_contact, base_dof, nj, 0...}
+ *   int32  parent[njoints], jtype[njoints] (0 universe, 1 free-flyer, 2 revolute),
+ *          idx_q[njoints], idx_v[njoints], contact_joint[n_contact], (one int32 pad if the count is odd)
+ *   double axis[njoints][3], placement_R[njoints][9] (row-major), placement_t[njoints][3],
+ *          contact_R[n_contact][9], contact_t[n_contact][3], gravity[3]
+ *
+ * Device panel layout (one row per generalized coordinate of every sample, row-major, ld >= W+1):
+ *   columns [0, Wy)            Y_proj        (Wy = 10·nb, pinocchio body order)
+ *           [Wy, Wy+nj)        B_v
+ *           [Wy+nj, W)         B_c            (W = Wy + 2·nj)
+ *           W                  tau_proj
+ *   The Gram buffer is the full symmetric (W+1)x(W+1) matrix panelᵀ·panel (row-major):
+ *   G[:W,:W] = AᵀA, G[:W,W] = Aᵀb, G[W,W] = bᵀb.
+ */
+#ifndef SYSID_H
+#define SYSID_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYSID_OK           0
+#define SYSID_E_INVALID   -1
+#define SYSID_E_MODEL     -2
+#define SYSID_E_DEVICE    -3
+#define SYSID_E_NOMEM     -4
+#define SYSID_E_CONTACT   -5
+
+#define SYSID_EMIT_Y        1u  /* stacked Y_proj                   */
+#define SYSID_EMIT_TAU      2u  /* stacked tau_proj                 */
+#define SYSID_EMIT_FRICTION 4u  /* stacked B_v and B_c              */
+#define SYSID_EMIT_GRAM     8u  /* G = panelᵀ panel (AᵀA, Aᵀb, bᵀb) */
+#define SYSID_EMIT_ALL     15u
+
+typedef struct sysid_engine sysid_engine;
+
+/* ABI version (bumped on any signature or layout change). */
+int32_t sysid_abi_version(void);
+
+/* Create an engine for one device from a packed model.  Replaces the model construction of
+ * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
+int32_t sysid_model_create(const void* packed_model, size_t nbytes, int32_t device, sysid_engine** out);
+void sysid_destroy(sysid_engine* e);
+
+/* Last error message of an engine, or of the calling thread when e == NULL. Never NULL. */
+const char* sysid_last_error(const sysid_engine* e);
+
+/* Model dimensions. panel_cols = W+1; panel_ld = default row stride of the device panel. */
+int32_t sysid_dims(const sysid_engine* e, int32_t* nq, int32_t* nv, int32_t* nj, int32_t* nb,
+                   int32_t* n_contact, int32_t* panel_cols, int32_t* panel_ld);
+
+/* Host-buffer entry point: the batched get_projected_y_tau + get_projected_friction_regressors
+ * (demo/spot_identification.py:37-56) followed by the stacking at :84-87 and the Gram.
+ *   q (nq x ld), dq/ddq (nv x ld), tau (nj x ld), cnt (n_contact x ld): float64, channel-major.
+ *   Y_proj (N·nv x 10·nb), tau_proj (N·nv), B_v/B_c (N·nv x nj): row-major, caller-allocated;
+ *   gram (W x W), Atb (W), btb (1).  Any output may be NULL ("don't emit"); flags select work.
+ * Synchronous: returns after all outputs are in host memory. */
+int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const double* ddq,
+                    const double* tau, const double* cnt, int64_t N, int64_t ld, uint32_t flags,
+                    double* Y_proj, double* tau_proj, double* B_v, double* B_c,
+                    double* gram, double* Atb, double* btb);
+
+/* Device workspace needed by sysid_build_device for N samples (bytes, 256-B aligned pieces). */
+size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags);
+
+/* Device-buffer entry point (stream-ordered, no host synchronisation, no allocation: graph-capturable).
+ *   d_in     : (nq + 2nv + nj + n_contact) x ld channel block [q; dq; ddq; tau; cnt], float64
+ *   d_panel  : (N·nv) x ld_panel panel (see layout above); always written
+ *   d_gram   : (W+1) x (W+1) Gram, written when flags & SYSID_EMIT_GRAM
+ *   stream   : hipStream_t, or NULL for the engine's own stream.
+ * Inputs are not validated on the device (see sysid_check_contacts). */
+int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
+                           double* d_panel, int64_t ld_panel, double* d_gram,
+                           void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* Host-side check of the contact contract for n_contact x ld contact values (SYSID_E_CONTACT on the
+ * first offending sample, whose index is written to *bad_sample when non-NULL). */
+int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld,
+                             int64_t* bad_sample);
+
+/* Kernel-only timing helper for bench.py: runs sysid_build_device `iters` times on the engine's
+ * stream bracketed by HIP events and returns the mean milliseconds per kernel of each stage:
+ * ms[0] = regressor/projector kernel, ms[1] = Gram kernel, ms[2] = Gram reduction kernel. */
+int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
+                          double* d_panel, int64_t ld_panel, double* d_gram,
+                          void* d_workspace, size_t workspace_bytes, int32_t iters, double* ms);
+
+/* Diagnostics: the host instantiation of the kernel's body-regressor column helper.
+ * body24 = {oR (9, row-major), ot (3), v (6, local [lin; ang]), a_gf (6, local)}; fw6 = column p (0..9)
+ * of pinocchio's bodyRegressor(v, a_gf) moved to the world frame.  Used by the CPU test-suite. */
+int32_t sysid_debug_body_column(const double* body24, int32_t p, double* fw6);
+/* LDS image of K1 for one sample (inputs as in sysid_build with N = ld = 1) after the projector / H
+ * phases; sysid_debug_layout gives the offsets {in, body, W, Pt, Jw, pf, Jc(=Q), L, M, P, H, total}. */
+int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq,
+                        const double* tau, const double* cnt, double* lds_image, int64_t image_doubles);
+int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12);
+/* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */
+int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SYSID_H */

@@ -1,0 +1,222 @@
+"""ctypes binding of libsysid.so (include/sysid.h).
+
+The product path has no CPU fallback: if the HIP library is missing, or no GPU is visible when a
+compute entry point is called, this module raises.  ``load_library()`` only loads the shared object
+(it is safe without a GPU; the CPU test-suite uses it to check the exported symbols).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .model import Model
+
+SYSID_OK = 0
+SYSID_E_INVALID = -1
+SYSID_E_MODEL = -2
+SYSID_E_DEVICE = -3
+SYSID_E_NOMEM = -4
+SYSID_E_CONTACT = -5
+
+EMIT_Y = 1
+EMIT_TAU = 2
+EMIT_FRICTION = 4
+EMIT_GRAM = 8
+EMIT_ALL = 15
+
+LIB_NAME = "libsysid.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+# (name, restype, argtypes) — one entry per function declared in include/sysid.h
+_c = ctypes
+_dp = _c.POINTER(_c.c_double)
+_vp = _c.c_void_p
+SIGNATURES = [
+    ("sysid_abi_version", _c.c_int32, []),
+    ("sysid_model_create", _c.c_int32, [_vp, _c.c_size_t, _c.c_int32, _c.POINTER(_vp)]),
+    ("sysid_destroy", None, [_vp]),
+    ("sysid_last_error", _c.c_char_p, [_vp]),
+    ("sysid_dims", _c.c_int32, [_vp] + [_c.POINTER(_c.c_int32)] * 7),
+    ("sysid_build", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _c.c_uint32,
+                                 _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    ("sysid_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64, _c.c_uint32]),
+    ("sysid_build_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64,
+                                        _vp, _vp, _c.c_size_t, _vp]),
+    ("sysid_check_contacts", _c.c_int32, [_vp, _dp, _c.c_int64, _c.c_int64, _c.POINTER(_c.c_int64)]),
+    ("sysid_debug_body_column", _c.c_int32, [_dp, _c.c_int32, _dp]),
+    ("sysid_debug_body_column_device", _c.c_int32, [_dp, _dp]),
+    ("sysid_debug_lds", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _c.c_int64]),
+    ("sysid_debug_layout", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
+    ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
+                                       _vp, _c.c_size_t, _c.c_int32, _dp]),
+]
+
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libsysid.so and declare every C-ABI signature.  Raises if the library is not built."""
+    global _LIB
+    if _LIB is not None and path == LIB_PATH:
+        return _LIB
+    # torch bundles its own libamdhip64.so.7; load it first so libsysid binds to the same HIP runtime
+    # (two runtimes in one process cannot share a device or a stream).
+    import torch  # noqa: F401
+    if not os.path.exists(path):
+        raise EngineError(
+            f"{path} is missing: the HIP engine is not built (run `python -c 'import __graft_entry__ as g; "
+            "g.build()'`).  There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _LIB = lib
+    return lib
+
+
+def _raise(code: int, msg: str):
+    if code in (SYSID_E_INVALID, SYSID_E_MODEL, SYSID_E_CONTACT):
+        raise ValueError(msg)
+    raise EngineError(msg)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_dp) if a is not None else None
+
+
+def _require_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        raise EngineError("no HIP device visible: the MI355X engine has no CPU fallback")
+
+
+class Engine:
+    """One model on one device.  Wraps ``sysid_engine*``."""
+
+    def __init__(self, model: Model, device: int = 0):
+        _require_gpu()
+        self.lib = load_library()
+        self.model = model
+        blob = model.pack()
+        self._blob = ctypes.create_string_buffer(blob, len(blob))
+        h = ctypes.c_void_p()
+        rc = self.lib.sysid_model_create(self._blob, len(blob), int(device), ctypes.byref(h))
+        if rc != SYSID_OK:
+            _raise(rc, self.lib.sysid_last_error(None).decode())
+        self._h = h
+        self.device = device
+        dims = [ctypes.c_int32() for _ in range(7)]
+        self.lib.sysid_dims(self._h, *[ctypes.byref(d) for d in dims])
+        self.nq, self.nv, self.nj, self.nb, self.n_contact, self.panel_cols, self.panel_ld = (d.value for d in dims)
+        self.wy = 10 * self.nb
+        self.w = self.wy + 2 * self.nj
+        self.in_rows = self.nq + 2 * self.nv + self.nj + self.n_contact
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.sysid_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != SYSID_OK:
+            _raise(rc, self.lib.sysid_last_error(self._h).decode())
+
+    # ---- host-buffer path --------------------------------------------------------------------
+    def build(self, q, dq, ddq, tau, cnt, flags: int = EMIT_ALL) -> dict:
+        """Channel-major (channels x N) inputs -> stacked outputs (+ Gram), all float64 numpy."""
+        ins = []
+        for a, rows, name in ((q, self.nq, "q"), (dq, self.nv, "dq"), (ddq, self.nv, "ddq"),
+                              (tau, self.nj, "tau"), (cnt, self.n_contact, "contact")):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+            if a.ndim == 1:
+                a = a.reshape(-1, 1)
+            if a.shape[0] != rows:
+                raise ValueError(f"{name}: expected {rows} channels, got shape {a.shape}")
+            ins.append(a)
+        N = ins[0].shape[1]
+        for a in ins:
+            if a.shape[1] != N:
+                raise ValueError("all inputs must have the same number of samples")
+        R = N * self.nv
+        out = {}
+        Y = np.empty((R, self.wy)) if flags & EMIT_Y else None
+        t = np.empty(R) if flags & EMIT_TAU else None
+        Bv = np.empty((R, self.nj)) if flags & EMIT_FRICTION else None
+        Bc = np.empty((R, self.nj)) if flags & EMIT_FRICTION else None
+        G = np.empty((self.w, self.w)) if flags & EMIT_GRAM else None
+        g = np.empty(self.w) if flags & EMIT_GRAM else None
+        btb = np.zeros(1) if flags & EMIT_GRAM else None
+        rc = self.lib.sysid_build(self._h, *[_ptr(a) for a in ins], N, N, int(flags),
+                                  _ptr(Y), _ptr(t), _ptr(Bv), _ptr(Bc), _ptr(G), _ptr(g), _ptr(btb))
+        self._check(rc)
+        if Y is not None:
+            out["Y_proj"] = Y
+        if t is not None:
+            out["tau_proj"] = t
+        if Bv is not None:
+            out["B_v"], out["B_c"] = Bv, Bc
+        if G is not None:
+            out["gram"], out["Atb"], out["btb"], out["num_rows"] = G, g, float(btb[0]), R
+        return out
+
+    # ---- device-buffer path (torch tensors on this engine's device) ----------------------------
+    def workspace_bytes(self, N: int, flags: int = EMIT_ALL) -> int:
+        return int(self.lib.sysid_workspace_bytes(self._h, int(N), int(flags)))
+
+    def alloc_device(self, N: int, flags: int = EMIT_ALL) -> dict:
+        import torch
+        dev = torch.device("cuda", self.device)
+        R = N * self.nv
+        return {
+            "panel": torch.empty((R, self.panel_ld), dtype=torch.float64, device=dev),
+            "gram": torch.empty((self.panel_cols, self.panel_cols), dtype=torch.float64, device=dev),
+            "ws": torch.empty(max(self.workspace_bytes(N, flags), 256), dtype=torch.uint8, device=dev),
+        }
+
+    def build_device(self, d_in, N: int, flags: int, bufs: dict, stream=None):
+        """Stream-ordered launch on device tensors.  ``d_in`` is the (in_rows x ld) channel block."""
+        import torch
+        if d_in.dtype != torch.float64 or not d_in.is_cuda or d_in.shape[0] != self.in_rows:
+            raise ValueError(f"d_in must be a float64 CUDA tensor with {self.in_rows} channel rows")
+        ld = d_in.stride(0)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.lib.sysid_build_device(
+            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(ld), int(flags),
+            ctypes.c_void_p(bufs["panel"].data_ptr()), int(bufs["panel"].stride(0)),
+            ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
+            int(bufs["ws"].numel()), ctypes.c_void_p(st))
+        self._check(rc)
+
+    def time_stages(self, d_in, N: int, flags: int, bufs: dict, iters: int = 10) -> list:
+        """Mean ms per kernel [regressor/projector, Gram SYRK, Gram reduce] (HIP events)."""
+        ms = np.zeros(3)
+        rc = self.lib.sysid_time_stages(
+            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)), int(flags),
+            ctypes.c_void_p(bufs["panel"].data_ptr()), int(bufs["panel"].stride(0)),
+            ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
+            int(bufs["ws"].numel()), int(iters), _ptr(ms))
+        self._check(rc)
+        return ms.tolist()
+
+    def views(self, bufs: dict, N: int) -> dict:
+        """Reference-shaped views of the device panel / Gram (no copies)."""
+        P = bufs["panel"][: N * self.nv]
+        G = bufs["gram"]
+        W = self.w
+        return {"Y_proj": P[:, : self.wy], "B_v": P[:, self.wy: self.wy + self.nj],
+                "B_c": P[:, self.wy + self.nj: W], "tau_proj": P[:, W],
+                "gram": G[:W, :W], "Atb": G[:W, W], "btb": G[W, W]}

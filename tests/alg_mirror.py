@@ -1,0 +1,99 @@
+"""numpy mirror of the HIP kernel's formulation (test helper, not product code).
+
+The kernel does not follow pinocchio's backward pass.  It uses, per sample:
+
+* world motion axes of every dof: ``w_r`` (direction) and ``p_r`` (point on the axis);
+* the contact Jacobian from the same axes; ``P = I - Q^T Q`` with ``Q = L^-1 J_c``, ``L L^T = J_c J_c^T``;
+* ``H_i = P · M_i · J_w^T`` (nv x 6, world coordinates), built by one rank-1 update per body from its
+  parent (``M_i`` = mask of the dofs supporting body i);
+* each regressor column of body i as ``H_i · f^w`` with ``f^w`` the body-regressor column moved to world.
+
+This file lets the test-suite check that formulation against the oracle on the CPU.
+"""
+import numpy as np
+
+from oracle import ref_numpy as ref
+
+JOINT_FREEFLYER = 1
+
+
+def world_axes(model, d):
+    nv = model.nv
+    W = np.zeros((nv, 3))
+    Pt = np.zeros((nv, 3))
+    lin = np.zeros(nv, dtype=bool)
+    for i in range(1, model.njoints):
+        iv = model.idx_v[i]
+        if model.jtypes[i] == JOINT_FREEFLYER:
+            for k in range(3):
+                W[iv + k] = d.oR[i][:, k]
+                lin[iv + k] = True
+                W[iv + 3 + k] = d.oR[i][:, k]
+                Pt[iv + 3 + k] = d.ot[i]
+        else:
+            W[iv] = d.oR[i] @ model.axes[i]
+            Pt[iv] = d.ot[i]
+    return W, Pt, lin
+
+
+def projector_cholqr(model, d, cnt, W, Pt, lin, tol=1e-12):
+    rows = []
+    for k, f in enumerate(model.contact_frames()):
+        if not cnt[k]:
+            continue
+        pf = d.oR[f.parent] @ f.t + d.ot[f.parent]
+        J = np.zeros((3, model.nv))
+        for r in model.support_dofs(f.parent):
+            J[:, r] = W[r] if lin[r] else np.cross(W[r], pf - Pt[r])
+        rows.append(J)
+    nv = model.nv
+    if not rows:
+        return np.eye(nv)
+    Jc = np.vstack(rows)
+    M = Jc @ Jc.T
+    k = M.shape[0]
+    L = np.zeros((k, k))
+    keep = np.ones(k, dtype=bool)
+    dmax = max(np.max(np.diag(M)), 1e-300)
+    for j in range(k):
+        s = M[j, j] - L[j, :j] @ L[j, :j]
+        if s <= tol * dmax:
+            keep[j] = False
+            continue
+        L[j, j] = np.sqrt(s)
+        for i in range(j + 1, k):
+            L[i, j] = (M[i, j] - L[i, :j] @ L[j, :j]) / L[j, j]
+    Q = np.zeros((k, nv))
+    for j in range(k):
+        if keep[j]:
+            Q[j] = (Jc[j] - L[j, :j] @ Q[:j]) / L[j, j]
+    return np.eye(nv) - Q.T @ Q
+
+
+def sample_panel(model, q, dq, ddq, tau, cnt):
+    """[Y_proj | B_v | B_c | tau_proj] for one sample via the kernel formulation."""
+    d = ref.forward_pass(model, q, dq, ddq)
+    W, Pt, lin = world_axes(model, d)
+    P = projector_cholqr(model, d, cnt, W, Pt, lin)
+    nv, nb = model.nv, model.nb
+    Jw = np.zeros((6, nv))  # world spatial axes [linear at origin; angular]
+    for r in range(nv):
+        Jw[:, r] = np.concatenate([W[r], np.zeros(3)]) if lin[r] else np.concatenate([np.cross(Pt[r], W[r]), W[r]])
+    H = [None] * model.njoints
+    for i in range(1, model.njoints):
+        par = model.parents[i]
+        Hi = np.zeros((nv, 6)) if par == 0 else H[par].copy()
+        iv = model.idx_v[i]
+        for r in range(iv, iv + model.nv_of(i)):
+            Hi += np.outer(P[:, r], Jw[:, r])
+        H[i] = Hi
+    Y = np.zeros((nv, 10 * nb))
+    for i in range(1, model.njoints):
+        bR = ref.body_regressor(d.v[i], d.a_gf[i])
+        Fw = ref.force_act(d.oR[i], d.ot[i], bR)  # local -> world
+        Y[:, 10 * (i - 1):10 * i] = H[i] @ Fw
+    bd = model.base_dof
+    Bv = P[:, bd:] * dq[bd:]
+    Bc = P[:, bd:] * np.sign(dq[bd:])
+    t = P[:, bd:] @ tau
+    return Y, t, Bv, Bc

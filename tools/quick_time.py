@@ -1,0 +1,22 @@
+"""Scratch timing of the three kernels (dev tool)."""
+import sys, os, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from system_identification_amd.engine import Engine, EMIT_ALL
+from system_identification_amd.model import load_robot
+from system_identification_amd.synthetic import generate, channel_block
+
+robot = sys.argv[1] if len(sys.argv) > 1 else "spot"
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
+m = load_robot(robot)
+d = generate(m, N, 1)
+eng = Engine(m)
+din = torch.from_numpy(channel_block(d)).cuda()
+bufs = eng.alloc_device(N, EMIT_ALL)
+eng.build_device(din, N, EMIT_ALL, bufs); torch.cuda.synchronize()
+ms = eng.time_stages(din, N, EMIT_ALL, bufs, iters=20)
+print(robot, N, "ms per kernel [K1, K2, K3]:", ["%.4f" % x for x in ms], "total %.4f" % sum(ms))
+bytes_k1 = N * ((m.nq + 2 * m.nv + m.nj + m.n_ee) * 8 + m.nv * (eng.w + 1) * 8)
+W = eng.w
+flops_k2 = N * (m.nv * W * (W + 1) + 2 * m.nv * W)
+print("K1 %.1f GB/s   K2 %.2f TF/s   samples/s %.3e" % (bytes_k1 / ms[0] / 1e6, flops_k2 / ms[1] / 1e9, N / sum(ms) * 1e3))
