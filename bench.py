@@ -1,0 +1,161 @@
+"""Benchmark: regressor + projector + Gram build on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--robot spot] [--samples 20000] [--gram-only]
+
+One "step" = one pass of the hot path over one batch of synthetic samples already resident in HBM:
+K1 (per-sample regressor Y, contact projector P, stacked [Y_proj | B_v | B_c | tau_proj] panel written
+to HBM in the reference's row layout) + K2/K3 (Gram AᵀA, Aᵀb, bᵀb on fp64 MFMA) + for N > 1 one RCCL
+all-reduce of the Gram.  Samples are sharded: every rank processes its own --samples (weak scaling).
+Rank 0 prints one JSON line.  For N > 1 launch with
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "regressor samples/sec + Gram-build GF/s, 12-DoF, 20k samples, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_MFMA_PEAK_TFS = 78.6  # AMD public spec for MI355X fp64 matrix (not in the container guide)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--robot", default="spot")
+    ap.add_argument("--samples", type=int, default=20000, help="samples per GPU")
+    ap.add_argument("--gram-only", action="store_true", help="skip nothing: panel still written (v1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="extra all-core C oracle timing (0 = off)")
+    return ap.parse_args()
+
+
+def cpu_baseline(model, data, n_sample):
+    """The C restatement of the reference path (oracle/sysid_oracle.c), one thread, on n_sample samples."""
+    from oracle.ref_c import COracle
+    o = COracle(model)
+    sl = {k: data[k][:, :n_sample].copy() for k in ("q", "dq", "ddq", "tau", "contact")}
+    t0 = time.perf_counter()
+    o.build(sl["q"], sl["dq"], sl["ddq"], sl["tau"], sl["contact"], nthreads=1)
+    dt = time.perf_counter() - t0
+    return n_sample / dt, dt
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from system_identification_amd.engine import EMIT_ALL, Engine
+    from system_identification_amd.model import load_robot
+    from system_identification_amd.synthetic import channel_block, generate
+
+    model = load_robot(args.robot)
+    N = args.samples
+    data = generate(model, N, config_index=1 + rank)  # each rank its own shard of the log
+    eng = Engine(model, device=local)
+    d_in = torch.from_numpy(channel_block(data)).cuda(local)
+    flags = EMIT_ALL
+    bufs = eng.alloc_device(N, flags)
+    stream = torch.cuda.current_stream(local)
+
+    def step():
+        eng.build_device(d_in, N, flags, bufs, stream=stream.cuda_stream)
+        if world > 1:
+            dist.all_reduce(bufs["gram"])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel device time (HIP events on the engine's stream), for the roofline
+    ms = eng.time_stages(d_in, N, flags, bufs, iters=max(5, args.steps))
+    nv, W = model.nv, eng.w
+    bytes_k1 = (model.nq + 2 * nv + model.nj + model.n_ee) * 8 + nv * (W + 1) * 8   # SURVEY §8d per sample
+    flops_k2 = nv * W * (W + 1) + 2 * nv * W                                       # SYRK + Aᵀb per sample
+    k1_gbs = N * bytes_k1 / (ms[0] * 1e-3) / 1e9
+    k2_tfs = N * flops_k2 / (ms[1] * 1e-3) / 1e12
+    if ms[0] >= ms[1]:
+        roof = {"kernel": "regressor_panel_kernel (K1)", "bound": "hbm", "achieved": round(k1_gbs, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
+                "traffic": None, "algorithmic_bytes_per_launch": N * bytes_k1,
+                "avg_launch_ms": round(ms[0], 5)}
+    else:
+        roof = {"kernel": "gram_syrk_kernel (K2)", "bound": "mfma", "achieved": round(k2_tfs, 3),
+                "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(k2_tfs / FP64_MFMA_PEAK_TFS, 4),
+                "traffic": None, "algorithmic_flops_per_launch": N * flops_k2,
+                "avg_launch_ms": round(ms[1], 5)}
+
+    total_samples = N * world * args.steps
+    value = total_samples / elapsed
+    result = {
+        "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8d recipe: sinusoidal joints in URDF limits, wobbling base, "
+                "inverse-dynamics torques + noise, trot contacts with LOST=2); no .dat ships with the reference",
+        "config": {"workload": f"{args.robot} {N} samples per GPU, full outputs (stacked Y_proj/tau_proj/"
+                               "B_v/B_c panel + Gram)", "robot": args.robot, "samples_per_gpu": N,
+                   "nv": nv, "W": W, "parallelism": f"dp{world}"},
+        "gram_gflops": round(N * world * flops_k2 / (elapsed / args.steps) / 1e9, 2),
+        "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
+                      "K3_gram_reduce": round(ms[2], 5)},
+        "K1_GBps": round(k1_gbs, 1), "K2_TFps": round(k2_tfs, 3),
+        "roofline": roof,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        n_cpu = min(N, 20000)
+        v, dt = cpu_baseline(model, data, n_cpu)
+        result["cpu_baseline"] = {
+            "value": round(v, 1), "unit": "samples/s", "cores": 1, "kind": "port",
+            "sample": f"{n_cpu} {args.robot} samples, oracle/sysid_oracle.c single thread: reference structure "
+                      f"(2 FK passes + 2 SVD pinv per sample, stacking, AᵀA), {dt:.2f} s",
+        }
+        if args.cpu_threads > 0:
+            from oracle.ref_c import COracle
+            o = COracle(model)
+            t0 = time.perf_counter()
+            o.build(data["q"], data["dq"], data["ddq"], data["tau"], data["contact"], nthreads=args.cpu_threads)
+            result["cpu_baseline_allcores"] = {"value": round(N / (time.perf_counter() - t0), 1),
+                                               "cores": args.cpu_threads}
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()
