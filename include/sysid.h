@@ -120,11 +120,13 @@ int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_
  * body24 = {oR (9, row-major), ot (3), v (6, local [lin; ang]), a_gf (6, local)}; fw6 = column p (0..9)
  * of pinocchio's bodyRegressor(v, a_gf) moved to the world frame.  Used by the CPU test-suite. */
 int32_t sysid_debug_body_column(const double* body24, int32_t p, double* fw6);
-/* LDS image of K1 for one sample (inputs as in sysid_build with N = ld = 1) after the projector / H
- * phases; sysid_debug_layout gives the offsets {in, body, W, Pt, Jw, pf, Jc(=Q), L, M, P, H, total}. */
+/* LDS image of K1 for one sample (inputs as in sysid_build with N = ld = 1) after the projector / H1
+ * phases; sysid_debug_layout gives the offsets {in, body, W, Pt, Jw, pf, Jc(=Q), M(=L), P, H1, tp, total}. */
 int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq,
                         const double* tau, const double* cnt, double* lds_image, int64_t image_doubles);
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12);
+/* K1 launch shape chosen at model creation: {waves per workgroup, workgroups per CU, LDS bytes, chain tpl}. */
+int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */
 int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6);
 

@@ -1,0 +1,695 @@
+// sysid_kernels.h — device code of the MI355X identification-regressor engine (gfx950, wave64).
+//
+// Included once, by sysid_engine.hip.  Kernels:
+//   k1_regressor_panel  per sample: forward kinematics, contact Jacobian, projector P, projected
+//                       regressor / friction / torque columns -> panel [Y_proj | B_v | B_c | tau_proj].
+//                       One wave = one sample; a workgroup holds 4 independent waves; no workgroup
+//                       barrier inside the sample loop (wave-synchronous LDS); persistent waves walk
+//                       contiguous sample ranges with the next sample's inputs prefetched.
+//   k2_gram_syrk        split-K SYRK of the panel on v_mfma_f64_16x16x4_f64 (upper 16x16 tiles),
+//                       8 waves, register-staged double-buffered row chunks in LDS.
+//   k3_gram_partial / k3_gram_final   deterministic two-level sum of the K2 slabs -> symmetric Gram.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sysid_dev {
+
+constexpr int JT_FREEFLYER = 1;
+constexpr int JT_REVOLUTE = 2;
+constexpr int K1_WAVES = 4;            // waves (= samples in flight) per K1 workgroup
+constexpr int K2_WAVES = 8;            // waves per K2 workgroup
+constexpr int K2_TPW = 7;              // Gram tiles per K2 wave (8 x 7 = 56 slots per group)
+constexpr int K2_PER = 8;              // max staged double2 per thread per chunk
+
+// ------------------------------------------------------------------------------------------------
+// layouts shared by host and device
+// ------------------------------------------------------------------------------------------------
+
+// Compact model image kept in LDS by every K1 workgroup.  Int section offsets are in 4-byte words,
+// double section offsets in doubles from the image start.
+struct MImg {
+  int parent, jtype, idx_q, idx_v, depth, chain_len, chain, dof_joint, dof_k, cjoint, csupp, nint;
+  int axis, R0, t0, ct, ndbl;
+};
+
+__host__ __device__ inline MImg mimg_layout(int NJ, int nv, int nc, int maxch) {
+  MImg m;
+  int o = 0;
+  m.parent = o; o += NJ;
+  m.jtype = o; o += NJ;
+  m.idx_q = o; o += NJ;
+  m.idx_v = o; o += NJ;
+  m.depth = o; o += NJ;
+  m.chain_len = o; o += NJ;
+  m.chain = o; o += NJ * maxch;
+  m.dof_joint = o; o += nv;
+  m.dof_k = o; o += nv;
+  m.cjoint = o; o += nc;
+  o = (o + 1) & ~1;
+  m.csupp = o; o += 2 * nc;
+  m.nint = o;
+  int d = o / 2;
+  m.axis = d; d += 3 * NJ;
+  m.R0 = d; d += 9 * NJ;
+  m.t0 = d; d += 3 * NJ;
+  m.ct = d; d += 3 * nc;
+  m.ndbl = (d + 1) & ~1;  // image size in doubles (16-B aligned)
+  return m;
+}
+
+// Per-wave LDS region of K1 (doubles, every piece 16-B aligned).
+struct WLay {
+  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, total;
+};
+
+__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc) {
+  WLay l;
+  const int k = 3 * nc;
+  int o = 0;
+  auto take = [&](int n) { const int r = o; o += (n + 1) & ~1; return r; };
+  l.in = take(in_rows);
+  l.body = take(NJ * 24);       // per joint: oR(9) ot(3) v(6) a_gf(6)
+  l.W = take(nv * 3);           // world direction of every dof's motion axis
+  l.Pt = take(nv * 3);          // a point on it
+  l.Jw = take(nv * 6);          // world spatial axis [linear at origin; angular]
+  l.pf = take(nc * 3);          // contact points (world)
+  l.Jc = take(k * nv);          // J_c, then Q = L^-1 J_c in place
+  l.M = take(k * k);            // J_c J_c^T, then its Cholesky factor in place
+  l.P = take(nv * nv);          // P = I - Q^T Q
+  l.H1 = take(nv * 6);          // P[:, ff] J_w[:, ff]^T
+  l.tp = take(nv);              // P S^T tau
+  l.total = o;
+  return l;
+}
+
+struct K1Params {
+  int nq, nv, NJ, nc, bd, nj, maxdepth, wy, w, ncol, in_rows, maxch, has_ff, ff0, mimg_dbl, wave_dbl;
+  int out_cols;     // columns written per panel row (ncol rounded up to the panel's even stride)
+  double thr_rel;   // Cholesky pivot cut (relative to max diag(J_c J_c^T))
+  double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
+};
+
+// ------------------------------------------------------------------------------------------------
+// small helpers (host+device so the CPU test-suite can exercise the same code)
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline void mat3mul(const double* A, const double* B, double* C) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+__host__ __device__ inline void mat3vec(const double* A, const double* x, double* y) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) y[i] = A[3 * i] * x[0] + A[3 * i + 1] * x[1] + A[3 * i + 2] * x[2];
+}
+
+__host__ __device__ inline void mat3tvec(const double* A, const double* x, double* y) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) y[i] = A[i] * x[0] + A[3 + i] * x[1] + A[6 + i] * x[2];
+}
+
+__host__ __device__ inline void cross3(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// SE3(R, t).actInv(motion m = [v; w])
+__host__ __device__ inline void act_inv_motion(const double* R, const double* t, const double* m, double* out) {
+  double tw[3], d[3];
+  cross3(t, m + 3, tw);
+  d[0] = m[0] - tw[0];
+  d[1] = m[1] - tw[1];
+  d[2] = m[2] - tw[2];
+  mat3tvec(R, d, out);
+  mat3tvec(R, m + 3, out + 3);
+}
+
+// Rotation about a unit axis; pinocchio's RX/RY/RZ closed forms for the aligned axes.
+__device__ inline void axis_rotation(const double* a, double ang, double* R) {
+  double s, c;
+  sincos(ang, &s, &c);
+  if (a[0] == 1.0 && a[1] == 0.0 && a[2] == 0.0) {
+    R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = c; R[5] = -s; R[6] = 0; R[7] = s; R[8] = c;
+  } else if (a[0] == 0.0 && a[1] == 1.0 && a[2] == 0.0) {
+    R[0] = c; R[1] = 0; R[2] = s; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = -s; R[7] = 0; R[8] = c;
+  } else if (a[0] == 0.0 && a[1] == 0.0 && a[2] == 1.0) {
+    R[0] = c; R[1] = -s; R[2] = 0; R[3] = s; R[4] = c; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+  } else {
+    const double C = 1.0 - c;
+    const double x = a[0], y = a[1], z = a[2];
+    R[0] = 1.0 + C * (x * x - 1.0); R[1] = -s * z + C * x * y;      R[2] = s * y + C * x * z;
+    R[3] = s * z + C * x * y;       R[4] = 1.0 + C * (y * y - 1.0); R[5] = -s * x + C * y * z;
+    R[6] = -s * y + C * x * z;      R[7] = s * x + C * y * z;       R[8] = 1.0 + C * (z * z - 1.0);
+  }
+}
+
+// Eigen Quaternion::toRotationMatrix (no normalisation), q = (x, y, z, w).
+__device__ inline void quat_to_matrix(double x, double y, double z, double w, double* R) {
+  const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w;
+  const double txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+  R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+__device__ inline double sign_of(double x) {
+  return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == x ? 0.0 : x));
+}
+
+// Column p of pinocchio's bodyRegressor(v, a_gf) (parameters [m, mc, Ixx, Ixy, Iyy, Ixz, Iyz, Izz];
+// force rows [f; n]) moved to the world frame: fw = oX_i^* f.  bi = {oR(9), ot(3), v(6), a_gf(6)}.
+// Branch-free: every lane of a wave runs the same instructions whatever its column p.
+__host__ __device__ inline void body_regressor_world_column(const double* bi, int p, double* fw) {
+  const double* v = bi + 12;
+  const double* a = bi + 18;
+  const double* w = v + 3;
+  const double* dw = a + 3;
+  double ac[3], tmp[3];
+  cross3(w, v, tmp);
+  ac[0] = a[0] + tmp[0]; ac[1] = a[1] + tmp[1]; ac[2] = a[2] + tmp[2];
+  const double sm = p == 0 ? 1.0 : 0.0;
+  const double e[3] = {p == 1 ? 1.0 : 0.0, p == 2 ? 1.0 : 0.0, p == 3 ? 1.0 : 0.0};
+  const double s0 = p == 4 ? 1.0 : 0.0, s1 = p == 5 ? 1.0 : 0.0, s2 = p == 6 ? 1.0 : 0.0;
+  const double s3 = p == 7 ? 1.0 : 0.0, s4 = p == 8 ? 1.0 : 0.0, s5 = p == 9 ? 1.0 : 0.0;
+  // f = m ac + (dw x + w x w x) h ;  n = h x ac + I dw + w x (I w)
+  double x1[3], x2[3], x3[3], n[3], f[3];
+  cross3(dw, e, x1);
+  cross3(w, e, x2);
+  cross3(w, x2, x3);
+  f[0] = sm * ac[0] + x1[0] + x3[0];
+  f[1] = sm * ac[1] + x1[1] + x3[1];
+  f[2] = sm * ac[2] + x1[2] + x3[2];
+  cross3(e, ac, n);
+  double bdw[3], bw[3];
+  bdw[0] = s0 * dw[0] + s1 * dw[1] + s3 * dw[2];
+  bdw[1] = s1 * dw[0] + s2 * dw[1] + s4 * dw[2];
+  bdw[2] = s3 * dw[0] + s4 * dw[1] + s5 * dw[2];
+  bw[0] = s0 * w[0] + s1 * w[1] + s3 * w[2];
+  bw[1] = s1 * w[0] + s2 * w[1] + s4 * w[2];
+  bw[2] = s3 * w[0] + s4 * w[1] + s5 * w[2];
+  cross3(w, bw, x2);
+  n[0] += bdw[0] + x2[0];
+  n[1] += bdw[1] + x2[1];
+  n[2] += bdw[2] + x2[2];
+  double nl[3];
+  mat3vec(bi, f, fw);
+  mat3vec(bi, n, nl);
+  cross3(bi + 9, fw, tmp);
+  fw[3] = nl[0] + tmp[0]; fw[4] = nl[1] + tmp[1]; fw[5] = nl[2] + tmp[2];
+}
+
+// Wave-level ordering point for LDS traffic.  The LDS executes one wave's DS instructions in issue
+// order, so a store by one lane is seen by a later load of any lane of the same wave; this only stops
+// the compiler from moving memory operations across the point.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+#ifdef SYSID_STAMPS
+#define K1_STAMP(k)                                                                                 \
+  if (lane == 0) {                                                                                  \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                     \
+    atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + (k), _t - t_prev);                      \
+    t_prev = _t;                                                                                    \
+  }
+#else
+#define K1_STAMP(k)
+#endif
+
+// ------------------------------------------------------------------------------------------------
+// K1
+// ------------------------------------------------------------------------------------------------
+template <int MAXCH>
+__global__ void __launch_bounds__(64 * K1_WAVES)
+k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
+                   int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp, double* __restrict__ dbg) {
+  extern __shared__ double smem[];
+  const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
+  {
+    uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
+    for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
+  }
+  __syncthreads();  // the only workgroup barrier: the model image is read-only from here on
+
+  const int* mi = reinterpret_cast<const int*>(smem);
+  const int* parent = mi + MI.parent;
+  const int* jtype = mi + MI.jtype;
+  const int* idx_q = mi + MI.idx_q;
+  const int* idx_v = mi + MI.idx_v;
+  const int* depth = mi + MI.depth;
+  const int* chain_len = mi + MI.chain_len;
+  const int* chain = mi + MI.chain;
+  const int* dof_joint = mi + MI.dof_joint;
+  const int* dof_k = mi + MI.dof_k;
+  const int* cjoint = mi + MI.cjoint;
+  const unsigned long long* csupp = reinterpret_cast<const unsigned long long*>(mi + MI.csupp);
+  const double* axis = smem + MI.axis;
+  const double* R0 = smem + MI.R0;
+  const double* t0 = smem + MI.t0;
+  const double* ct = smem + MI.ct;
+
+  const int nv = kp.nv, nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const WLay L = wave_layout(IN, nv, NJ, nc);
+  double* wr = smem + kp.mimg_dbl + wave * kp.wave_dbl;
+  double* sin_ = wr + L.in;
+  const double* q = sin_;
+  const double* dq = sin_ + nq;
+  const double* ddq = dq + nv;
+  const double* tau = ddq + nv;
+  const double* cnt = tau + nja;
+  double* body = wr + L.body;
+  double* Ws = wr + L.W;
+  double* Pts = wr + L.Pt;
+  double* Jws = wr + L.Jw;
+  double* pfs = wr + L.pf;
+  double* Jc = wr + L.Jc;
+  double* Ms = wr + L.M;
+  double* Ps = wr + L.P;
+  double* H1 = wr + L.H1;
+  double* tps = wr + L.tp;
+
+  const int wpb = blockDim.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * wpb + wave;
+  const int64_t TW = (int64_t)gridDim.x * wpb;
+  const int64_t s_begin = gw * N / TW, s_end = (gw + 1) * N / TW;
+  if (s_begin >= s_end) return;  // no workgroup barrier follows
+
+  // inputs of the next sample are prefetched into registers (channel c -> lane c, c+64, c+128)
+  double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+  auto fetch = [&](int64_t s) {
+    if (lane < IN) x0 = in[(int64_t)lane * ld + s];
+    if (lane + 64 < IN) x1 = in[(int64_t)(lane + 64) * ld + s];
+    if (lane + 128 < IN) x2 = in[(int64_t)(lane + 128) * ld + s];
+  };
+  fetch(s_begin);
+#ifdef SYSID_STAMPS
+  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
+
+  for (int64_t s = s_begin; s < s_end; ++s) {
+    wsync();
+    if (lane < IN) sin_[lane] = x0;
+    if (lane + 64 < IN) sin_[lane + 64] = x1;
+    if (lane + 128 < IN) sin_[lane + 128] = x2;
+    if (lane < 24) {
+      double v = 0.0;
+      if (lane == 0 || lane == 4 || lane == 8) v = 1.0;   // oR_0 = I
+      if (lane >= 18 && lane < 21) v = -(lane == 18 ? kp.g0 : (lane == 19 ? kp.g1 : kp.g2));
+      body[lane] = v;
+    }
+    if (s + 1 < s_end) fetch(s + 1);
+    wsync();
+    K1_STAMP(0)
+
+    // ---- forward pass (computeJointTorqueRegressor forward step) + world placements ----
+    for (int lvl = 1; lvl <= kp.maxdepth; ++lvl) {
+      for (int j = 1 + lane; j < NJ; j += 64) {
+        if (depth[j] != lvl) continue;
+        const int p = parent[j];
+        const int iq = idx_q[j], iv = idx_v[j];
+        const double* bp = body + 24 * p;
+        double* bj = body + 24 * j;
+        double RJ[9], tJ[3], vJ[6], Sa[6];
+        const bool ff = jtype[j] == JT_FREEFLYER;
+        if (ff) {
+          quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], RJ);
+          tJ[0] = q[iq]; tJ[1] = q[iq + 1]; tJ[2] = q[iq + 2];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) { vJ[k] = dq[iv + k]; Sa[k] = ddq[iv + k]; }
+        } else {
+          const double* ax = axis + 3 * j;
+          axis_rotation(ax, q[iq], RJ);
+          tJ[0] = tJ[1] = tJ[2] = 0.0;
+          const double w = dq[iv], aa = ddq[iv];
+          vJ[0] = vJ[1] = vJ[2] = 0.0; Sa[0] = Sa[1] = Sa[2] = 0.0;
+          vJ[3] = ax[0] * w; vJ[4] = ax[1] * w; vJ[5] = ax[2] * w;
+          Sa[3] = ax[0] * aa; Sa[4] = ax[1] * aa; Sa[5] = ax[2] * aa;
+        }
+        double liR[9], lit[3], tmp[3];
+        mat3mul(R0 + 9 * j, RJ, liR);
+        mat3vec(R0 + 9 * j, tJ, tmp);
+        lit[0] = tmp[0] + t0[3 * j]; lit[1] = tmp[1] + t0[3 * j + 1]; lit[2] = tmp[2] + t0[3 * j + 2];
+        double vp[6], ap[6], vi[6], ai[6], c1[3], c2[3];
+        act_inv_motion(liR, lit, bp + 12, vp);
+        act_inv_motion(liR, lit, bp + 18, ap);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) vi[k] = vJ[k] + vp[k];
+        if (ff) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) ai[k] = Sa[k] + ap[k];  // v x v = 0
+        } else {
+          cross3(vi, vJ + 3, c1);      // motion cross v x vJ with vJ = (0, wJ)
+          cross3(vi + 3, vJ + 3, c2);
+          ai[0] = c1[0] + Sa[0] + ap[0]; ai[1] = c1[1] + Sa[1] + ap[1]; ai[2] = c1[2] + Sa[2] + ap[2];
+          ai[3] = c2[0] + Sa[3] + ap[3]; ai[4] = c2[1] + Sa[4] + ap[4]; ai[5] = c2[2] + Sa[5] + ap[5];
+        }
+        double oR[9], ot[3];
+        mat3mul(bp, liR, oR);
+        mat3vec(bp, lit, ot);
+        ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) bj[k] = oR[k];
+        bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { bj[12 + k] = vi[k]; bj[18 + k] = ai[k]; }
+      }
+      wsync();
+    }
+    K1_STAMP(1)
+
+    // ---- world motion axes of every dof; contact points ----
+    for (int e = lane; e < nv + nc; e += 64) {
+      if (e < nv) {
+        const int r = e;
+        const int j = dof_joint[r];
+        const double* bj = body + 24 * j;
+        double W[3], P[3] = {bj[9], bj[10], bj[11]};
+        bool lin = false;
+        if (jtype[j] == JT_FREEFLYER) {
+          const int k = dof_k[r];
+          const int col = k < 3 ? k : k - 3;
+          W[0] = bj[col]; W[1] = bj[3 + col]; W[2] = bj[6 + col];
+          lin = k < 3;
+        } else {
+          mat3vec(bj, axis + 3 * j, W);
+        }
+        Ws[3 * r] = W[0]; Ws[3 * r + 1] = W[1]; Ws[3 * r + 2] = W[2];
+        Pts[3 * r] = P[0]; Pts[3 * r + 1] = P[1]; Pts[3 * r + 2] = P[2];
+        double* jw = Jws + 6 * r;
+        if (lin) {
+          jw[0] = W[0]; jw[1] = W[1]; jw[2] = W[2]; jw[3] = 0.0; jw[4] = 0.0; jw[5] = 0.0;
+        } else {
+          double pw[3];
+          cross3(P, W, pw);
+          jw[0] = pw[0]; jw[1] = pw[1]; jw[2] = pw[2]; jw[3] = W[0]; jw[4] = W[1]; jw[5] = W[2];
+        }
+      } else {
+        const int c = e - nv;
+        const double* bj = body + 24 * cjoint[c];
+        double x[3];
+        mat3vec(bj, ct + 3 * c, x);
+        pfs[3 * c] = x[0] + bj[9]; pfs[3 * c + 1] = x[1] + bj[10]; pfs[3 * c + 2] = x[2] + bj[11];
+      }
+    }
+    int na = 0;
+    for (int c = 0; c < nc; ++c) na += cnt[c] != 0.0 ? 1 : 0;
+    const int k = 3 * na;
+    wsync();
+    K1_STAMP(2)
+
+    // ---- contact Jacobian (LOCAL_WORLD_ALIGNED, linear rows) ----
+    for (int e = lane; e < k * nv; e += 64) {
+      const int rho = e / nv, r = e - rho * nv;
+      int c = 0;
+      for (int seen = -1; c < nc; ++c) {  // the (rho/3)-th contact with a non-zero value
+        seen += cnt[c] != 0.0 ? 1 : 0;
+        if (seen == rho / 3) break;
+      }
+      const int comp = rho - 3 * (rho / 3);
+      double val = 0.0;
+      if ((csupp[c] >> r) & 1ull) {
+        const double* W = Ws + 3 * r;
+        if (jtype[dof_joint[r]] == JT_FREEFLYER && dof_k[r] < 3) {
+          val = W[comp];
+        } else {
+          double d[3], x[3];
+          d[0] = pfs[3 * c] - Pts[3 * r];
+          d[1] = pfs[3 * c + 1] - Pts[3 * r + 1];
+          d[2] = pfs[3 * c + 2] - Pts[3 * r + 2];
+          cross3(W, d, x);
+          val = x[comp];
+        }
+      }
+      Jc[rho * nv + r] = val;
+    }
+    wsync();
+
+    // ---- M = J_c J_c^T ----
+    for (int e = lane; e < k * k; e += 64) {
+      const int a = e / k, b = e - a * k;
+      double acc = 0.0;
+      for (int r = 0; r < nv; ++r) acc += Jc[a * nv + r] * Jc[b * nv + r];
+      Ms[e] = acc;
+    }
+    wsync();
+    K1_STAMP(3)
+
+    // ---- in-place Cholesky of M (right-looking); pivots <= thr_rel * max diag are dropped ----
+    {
+      double dmax = 0.0;
+      for (int a = 0; a < k; ++a) dmax = fmax(dmax, Ms[a * k + a]);
+      const double thr = kp.thr_rel * dmax;
+      for (int j = 0; j < k; ++j) {
+        const double djj = Ms[j * k + j];
+        wsync();
+        const bool keep = djj > thr;
+        const double ljj = keep ? sqrt(djj) : 0.0;
+        for (int i = j + lane; i < k; i += 64)
+          Ms[i * k + j] = !keep ? 0.0 : (i == j ? ljj : Ms[i * k + j] / ljj);
+        wsync();
+        const int rem = k - j - 1;
+        for (int e = lane; e < rem * rem; e += 64) {
+          const int i = j + 1 + e / rem, l = j + 1 + e % rem;
+          if (l <= i) Ms[i * k + l] -= Ms[i * k + j] * Ms[l * k + j];
+        }
+        wsync();
+      }
+    }
+    K1_STAMP(4)
+
+    // ---- Q = L^-1 J_c (one column per lane, in place) ----
+    for (int r = lane; r < nv; r += 64) {
+      for (int j = 0; j < k; ++j) {
+        const double ljj = Ms[j * k + j];
+        double x = Jc[j * nv + r];
+        for (int l = 0; l < j; ++l) x -= Ms[j * k + l] * Jc[l * nv + r];
+        Jc[j * nv + r] = ljj != 0.0 ? x / ljj : 0.0;
+      }
+    }
+    wsync();
+
+    // ---- P = I - Q^T Q ----
+    for (int e = lane; e < nv * nv; e += 64) {
+      const int a = e / nv, b = e - a * nv;
+      double acc = 0.0;
+      for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Jc[j * nv + b];
+      Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+    }
+    wsync();
+    K1_STAMP(5)
+
+    // ---- H1 = P[:, ff] J_w[:, ff]^T ;  tp = P S^T tau ----
+    for (int e = lane; e < nv * 7; e += 64) {
+      if (e < nv * 6) {
+        const int r = e / 6, c = e - 6 * r;
+        double h = 0.0;
+        if (kp.has_ff)
+          for (int d = 0; d < 6; ++d) h += Ps[r * nv + kp.ff0 + d] * Jws[6 * (kp.ff0 + d) + c];
+        H1[e] = h;
+      } else {
+        const int r = e - nv * 6;
+        double acc = 0.0;
+        for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
+        tps[r] = acc;
+      }
+    }
+    wsync();
+    if (dbg != nullptr && s == 0) {
+#ifndef SYSID_STAMPS
+      for (int x = lane; x < L.total; x += 64) dbg[x] = wr[x];  // diagnostics: LDS image of sample 0
+#endif
+    }
+    K1_STAMP(6)
+
+    // ---- panel columns: [Y_proj | B_v | B_c | tau_proj | pad] ----
+    double* out = panel + (s * nv) * ldp;
+    for (int col = lane; col < kp.out_cols; col += 64) {
+      if (col < kp.wy) {
+        const int i = col / 10 + 1, p = col - 10 * (col / 10);
+        double fw[6];
+        body_regressor_world_column(body + 24 * i, p, fw);
+        // revolute ancestors of body i (and i): c_t = J_w[:, dof_t] . fw
+        const int cl = chain_len[i];
+        int dof[MAXCH];
+        double cv[MAXCH];
+#pragma unroll
+        for (int t = 0; t < MAXCH; ++t) {
+          dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
+          const double* jw = Jws + 6 * dof[t];
+          cv[t] = t < cl ? jw[0] * fw[0] + jw[1] * fw[1] + jw[2] * fw[2] + jw[3] * fw[3] + jw[4] * fw[4] +
+                               jw[5] * fw[5]
+                         : 0.0;
+        }
+        for (int r = 0; r < nv; ++r) {
+          const double* h = H1 + 6 * r;
+          double acc = h[0] * fw[0] + h[1] * fw[1] + h[2] * fw[2] + h[3] * fw[3] + h[4] * fw[4] + h[5] * fw[5];
+          const double* pr = Ps + r * nv;
+#pragma unroll
+          for (int t = 0; t < MAXCH; ++t)
+            if (t < cl) acc += pr[dof[t]] * cv[t];
+          out[(int64_t)r * ldp + col] = acc;
+        }
+      } else if (col < kp.wy + 2 * nja) {
+        const bool coul = col >= kp.wy + nja;
+        const int jj = col - kp.wy - (coul ? nja : 0);
+        const double x = dq[bd + jj];
+        const double sc = coul ? sign_of(x) : x;
+        for (int r = 0; r < nv; ++r) out[(int64_t)r * ldp + col] = Ps[r * nv + bd + jj] * sc;
+      } else if (col == kp.w) {
+        for (int r = 0; r < nv; ++r) out[(int64_t)r * ldp + col] = tps[r];
+      } else {
+        for (int r = 0; r < nv; ++r) out[(int64_t)r * ldp + col] = 0.0;  // pad: keep lines whole
+      }
+    }
+    K1_STAMP(7)
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2: G_partial[ks] = panel[rows of ks]^T panel[rows of ks]   (fp64 MFMA 16x16x4, upper tiles)
+// ------------------------------------------------------------------------------------------------
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(64 * K2_WAVES)
+k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, int ncol, int ntc, int stride,
+             int kc, const int2* __restrict__ tiles, int ngroups, int ksplit, int nslots,
+             double* __restrict__ slab) {
+  extern __shared__ double buf[];  // 2 x kc x stride
+  const int group = blockIdx.x % ngroups;
+  const int ks = blockIdx.x / ngroups;
+  const int64_t r0 = rows * ks / ksplit, r1 = rows * (ks + 1) / ksplit;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int slot0 = (group * K2_WAVES + wave) * K2_TPW;
+  int tI[K2_TPW], tJ[K2_TPW];
+#pragma unroll
+  for (int t = 0; t < K2_TPW; ++t) {
+    const int2 ij = tiles[slot0 + t];
+    tI[t] = ij.x;
+    tJ[t] = ij.y;
+  }
+  dbl4 acc[K2_TPW];
+#pragma unroll
+  for (int t = 0; t < K2_TPW; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  const int half = ntc * 8;  // double2 per staged row
+  const int pairs = kc * half;
+  double2 st[K2_PER];
+  auto load_chunk = [&](int64_t c0) {
+#pragma unroll
+    for (int u = 0; u < K2_PER; ++u) {
+      const int e = threadIdx.x + u * 64 * K2_WAVES;
+      double2 v = {0.0, 0.0};
+      if (e < pairs) {
+        const int rr = e / half, col = 2 * (e - rr * half);
+        const int64_t g = c0 + rr;
+        if (g < r1 && col < ncol) {
+          v = *reinterpret_cast<const double2*>(panel + g * ldp + col);
+          if (col + 1 >= ncol) v.y = 0.0;
+        }
+      }
+      st[u] = v;
+    }
+  };
+  auto store_chunk = [&](double* b) {
+#pragma unroll
+    for (int u = 0; u < K2_PER; ++u) {
+      const int e = threadIdx.x + u * 64 * K2_WAVES;
+      if (e < pairs) {
+        const int rr = e / half, col = 2 * (e - rr * half);
+        *reinterpret_cast<double2*>(b + rr * stride + col) = st[u];
+      }
+    }
+  };
+  const int64_t nchunks = (r1 - r0 + kc - 1) / kc;
+  const int kr = lane >> 4, k16 = lane & 15;
+  if (nchunks > 0) {
+    load_chunk(r0);
+    store_chunk(buf);
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < nchunks; ++c) {
+    double* cur = buf + (c & 1) * kc * stride;
+    double* nxt = buf + ((c + 1) & 1) * kc * stride;
+    if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * kc);
+    for (int kk = 0; kk < kc; kk += 4) {
+      const double* rowp = cur + (kk + kr) * stride + k16;
+      double a[K2_TPW], b[K2_TPW];
+#pragma unroll
+      for (int t = 0; t < K2_TPW; ++t) {
+        a[t] = tI[t] >= 0 ? rowp[tI[t] * 16] : 0.0;
+        b[t] = tI[t] >= 0 ? rowp[tJ[t] * 16] : 0.0;
+      }
+#pragma unroll
+      for (int t = 0; t < K2_TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
+    }
+    if (c + 1 < nchunks) store_chunk(nxt);
+    __syncthreads();
+  }
+  // D layout of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int t = 0; t < K2_TPW; ++t) {
+    if (tI[t] < 0) continue;
+    double* o = slab + ((size_t)ks * nslots + slot0 + t) * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[((lane >> 4) + 4 * j) * 16 + (lane & 15)] = acc[t][j];
+  }
+}
+
+// K3a: part[r][x] = sum of slab[ks][x] over ks in split r  (x = slot*256 + element)
+__global__ void __launch_bounds__(256)
+k3_gram_partial(const double* __restrict__ slab, int64_t nx, int ksplit, int rsplit, double* __restrict__ part) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y;
+  if (x >= nx) return;
+  const int k0 = ksplit * r / rsplit, k1 = ksplit * (r + 1) / rsplit;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int ks = k0;
+  for (; ks + 4 <= k1; ks += 4) {
+    a0 += slab[(size_t)ks * nx + x];
+    a1 += slab[(size_t)(ks + 1) * nx + x];
+    a2 += slab[(size_t)(ks + 2) * nx + x];
+    a3 += slab[(size_t)(ks + 3) * nx + x];
+  }
+  for (; ks < k1; ++ks) a0 += slab[(size_t)ks * nx + x];
+  part[(size_t)r * nx + x] = (a0 + a1) + (a2 + a3);
+}
+
+// K3b: G[I*16+r][J*16+c] = sum_r part[r][slot][r*16+c], mirrored.
+__global__ void __launch_bounds__(256)
+k3_gram_final(const double* __restrict__ part, const int2* __restrict__ tiles, int nslots, int rsplit, int ncol,
+              double* __restrict__ G) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nx = (int64_t)nslots * 256;
+  if (e >= nx) return;
+  const int t = (int)(e >> 8), x = (int)(e & 255);
+  const int2 ij = tiles[t];
+  if (ij.x < 0) return;
+  double acc = 0.0;
+  for (int r = 0; r < rsplit; ++r) acc += part[(size_t)r * nx + e];
+  const int gi = ij.x * 16 + (x >> 4), gj = ij.y * 16 + (x & 15);
+  if (gi < ncol && gj < ncol) {
+    G[(int64_t)gi * ncol + gj] = acc;
+    G[(int64_t)gj * ncol + gi] = acc;
+  }
+}
+
+// Diagnostics kernel: lane l computes column (l % 10) of the body regressor in world frame.
+__global__ void debug_body_column_kernel(const double* __restrict__ body24, double* __restrict__ out) {
+  __shared__ double b[24];
+  if (threadIdx.x < 24) b[threadIdx.x] = body24[threadIdx.x];
+  __syncthreads();
+  double fw[6];
+  body_regressor_world_column(b, threadIdx.x % 10, fw);
+  for (int k = 0; k < 6; ++k) out[threadIdx.x * 6 + k] = fw[k];
+}
+
+}  // namespace sysid_dev

@@ -49,6 +49,7 @@ SIGNATURES = [
     ("sysid_debug_body_column_device", _c.c_int32, [_dp, _dp]),
     ("sysid_debug_lds", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _c.c_int64]),
     ("sysid_debug_layout", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
+    ("sysid_debug_k1_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
 ]
