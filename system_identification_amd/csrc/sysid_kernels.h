@@ -352,10 +352,20 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           ai[0] = c1[0] + Sa[0] + ap[0]; ai[1] = c1[1] + Sa[1] + ap[1]; ai[2] = c1[2] + Sa[2] + ap[2];
           ai[3] = c2[0] + Sa[3] + ap[3]; ai[4] = c2[1] + Sa[4] + ap[4]; ai[5] = c2[2] + Sa[5] + ap[5];
         }
+        // Poses are kept relative to the free-flyer (base) frame, not the world: the regressor rows of
+        // pinocchio only see the base rotation through R_b^T g (its actInv above), and J_c's row space
+        // (hence P) is the same in base-aligned and world-aligned axes because R_b is invertible.  This
+        // stays exact for the float32, slightly non-unit quaternions of the reference's .dat logs.
         double oR[9], ot[3];
-        mat3mul(bp, liR, oR);
-        mat3vec(bp, lit, ot);
-        ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
+        if (ff) {
+          oR[0] = 1.0; oR[1] = 0.0; oR[2] = 0.0; oR[3] = 0.0; oR[4] = 1.0; oR[5] = 0.0;
+          oR[6] = 0.0; oR[7] = 0.0; oR[8] = 1.0;
+          ot[0] = ot[1] = ot[2] = 0.0;
+        } else {
+          mat3mul(bp, liR, oR);
+          mat3vec(bp, lit, ot);
+          ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
+        }
 #pragma unroll
         for (int k = 0; k < 9; ++k) bj[k] = oR[k];
         bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];

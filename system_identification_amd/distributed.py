@@ -1,0 +1,74 @@
+"""Multi-GPU normal equations: samples sharded over ranks, one all-reduce of the Gram.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on ROCm).  Rank r owns the
+contiguous samples ``[r·N/G, (r+1)·N/G)`` (filtering is done on the host first, so no halo), builds its
+partial Gram on its own device, and a single ``all_reduce(SUM)`` of the (W+1)x(W+1) fp64 buffer gives
+every rank the full normal equations.  The stacked Y panel, if requested, stays sharded.
+
+The per-rank compute is a parameter (``build_partial``) so the same host logic runs with the HIP engine
+on a GPU and, in the CPU test-suite, with a checker under the gloo backend.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import numpy as np
+
+
+def shard_range(N: int, rank: int, world: int) -> tuple:
+    """Contiguous sample range of ``rank`` (sizes differ by at most one)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    return (N * rank) // world, (N * (rank + 1)) // world
+
+
+def shard_channels(arrays, rank: int, world: int):
+    """Slice channel-major (channels x N) arrays to this rank's samples."""
+    N = np.asarray(arrays[0]).shape[-1]
+    s0, s1 = shard_range(N, rank, world)
+    return [np.ascontiguousarray(np.asarray(a)[..., s0:s1]) for a in arrays]
+
+
+def pack_normal_equations(ne: dict):
+    """(W+1)x(W+1) buffer [[G, g], [gᵀ, bᵀb]] and the row count (the engine's device Gram layout)."""
+    G, g = np.asarray(ne["gram"]), np.asarray(ne["Atb"])
+    W = G.shape[0]
+    buf = np.empty((W + 1, W + 1))
+    buf[:W, :W] = G
+    buf[:W, W] = g
+    buf[W, :W] = g
+    buf[W, W] = ne["btb"]
+    return buf, int(ne["num_rows"])
+
+
+def unpack_normal_equations(buf, num_rows: int) -> dict:
+    buf = np.asarray(buf)
+    W = buf.shape[0] - 1
+    return {"gram": buf[:W, :W].copy(), "Atb": buf[:W, W].copy(), "btb": float(buf[W, W]), "num_rows": int(num_rows)}
+
+
+def allreduce_normal_equations(ne: dict, device=None, group=None) -> dict:
+    """Sum the per-rank normal equations over the process group (one collective of the packed buffer
+    plus the row count riding in the same buffer's spare element)."""
+    import torch
+    import torch.distributed as dist
+    buf, rows = pack_normal_equations(ne)
+    W1 = buf.shape[0]
+    flat = np.concatenate([buf.reshape(-1), [float(rows)]])
+    t = torch.from_numpy(flat)
+    if device is not None:
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    out = t.cpu().numpy()
+    return unpack_normal_equations(out[:-1].reshape(W1, W1), int(round(out[-1])))
+
+
+def build_normal_equations_distributed(q, dq, ddq, tau, cnt, build_partial: Callable, rank: int, world: int,
+                                       device=None, group=None) -> dict:
+    """Shard (channel-major) inputs, build this rank's partial normal equations with ``build_partial``
+    (e.g. ``SystemIdentification.build_normal_equations``), and all-reduce them."""
+    parts = shard_channels([q, dq, ddq, tau, cnt], rank, world)
+    ne = build_partial(*parts)
+    if world == 1:
+        return ne
+    return allreduce_normal_equations(ne, device=device, group=group)

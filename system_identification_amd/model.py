@@ -127,6 +127,9 @@ class Model:
     link_visuals: list = field(default_factory=list)
     lower: list = field(default_factory=list)   # URDF joint limits (nan for universe / free-flyer)
     upper: list = field(default_factory=list)
+    # bounding ellipsoids of the listed links' visuals (src/sys_identification.py:235-264), computed when
+    # the model is compiled next to its meshes; None entries mark meshes that are not available
+    bounding_ellipsoids: list = field(default_factory=list)
     # robot YAML (files/*/<robot>_config.yaml)
     robot_name: str = ""
     robot_mass: float = 0.0
@@ -240,6 +243,9 @@ class Model:
             "robot": {"name": self.robot_name, "mass": self.robot_mass,
                       "end_effectors_frame_names": self.end_effector_names,
                       "link_names": self.link_names},
+            "bounding_ellipsoids": [None if e is None else {"link": e["link"], "semi_axes": list(map(float, e["semi_axes"])),
+                                                            "center": list(map(float, e["center"]))}
+                                    for e in self.bounding_ellipsoids],
             "lower": [None if not np.isfinite(x) else x for x in self.lower],
             "upper": [None if not np.isfinite(x) else x for x in self.upper],
             "gravity": list(self.gravity),
@@ -267,6 +273,9 @@ class Model:
             robot_name=rob.get("name", ""), robot_mass=rob.get("mass", 0.0),
             end_effector_names=list(rob.get("end_effectors_frame_names", [])),
             link_names=list(rob.get("link_names", [])),
+            bounding_ellipsoids=[None if e is None else {"link": e["link"], "semi_axes": np.array(e["semi_axes"]),
+                                                         "center": np.array(e["center"])}
+                                 for e in d.get("bounding_ellipsoids", [])],
             lower=[np.nan if x is None else x for x in d.get("lower", [])],
             upper=[np.nan if x is None else x for x in d.get("upper", [])],
             gravity=tuple(d.get("gravity", GRAVITY)),
@@ -337,6 +346,62 @@ def _link_visuals(link) -> list:
             out.append(LinkVisual(name, "sphere", [float(geo.find("sphere").get("radius"))], xyz))
         elif geo.find("mesh") is not None:
             out.append(LinkVisual(name, "mesh", [], xyz, geo.find("mesh").get("filename", "")))
+    return out
+
+
+def mesh_aabb(path: str) -> tuple:
+    """(min, max) corners of the vertices of an OBJ or STL (ascii/binary) mesh file."""
+    with open(path, "rb") as fh:
+        raw = fh.read()
+    ext = os.path.splitext(path)[1].lower()
+    if ext == ".obj":
+        pts = [list(map(float, ln.split()[1:4])) for ln in raw.decode(errors="ignore").splitlines()
+               if ln.startswith("v ")]
+        V = np.array(pts, dtype=float)
+    elif ext == ".stl":
+        n = struct.unpack_from("<I", raw, 80)[0] if len(raw) >= 84 else -1
+        if len(raw) == 84 + 50 * n:
+            rec = np.frombuffer(raw, dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]),
+                                count=n, offset=84)
+            V = rec["v"].reshape(-1, 3).astype(float)
+        else:
+            V = np.array([list(map(float, ln.split()[1:4])) for ln in raw.decode(errors="ignore").splitlines()
+                          if ln.strip().startswith("vertex")], dtype=float)
+    else:
+        raise ValueError(f"unsupported mesh format: {path}")
+    if V.size == 0:
+        raise ValueError(f"no vertices in {path}")
+    return V.min(axis=0), V.max(axis=0)
+
+
+def bounding_ellipsoids(model: "Model", urdf_file: str, mesh_root: str | None = None) -> list:
+    """Restates ``_compute_bounding_ellipsoids`` (src/sys_identification.py:235-264): for every visual of
+    every URDF link listed in the robot YAML, in URDF order, an axis-aligned ellipsoid.
+    Box: semi-axes size/2; cylinder: (r, r, l/2); sphere: (r, r, r); all centred at the visual origin.
+    Mesh: semi-axes = AABB extents / 2, centre = AABB centre + visual origin.  The reference resolves
+    ``filename[10:]`` (strips "package://") under ``files/``; here ``mesh_root`` plays that role and
+    plain relative paths resolve next to the URDF.  A missing mesh file gives a ``None`` entry."""
+    out = []
+    root = mesh_root or os.path.dirname(os.path.dirname(os.path.abspath(urdf_file)))
+    for v in model.link_visuals:
+        if v.link not in model.link_names:
+            continue
+        if v.kind == "box":
+            semi, center = np.asarray(v.params) / 2.0, np.asarray(v.xyz, dtype=float)
+        elif v.kind == "cylinder":
+            semi, center = np.array([v.params[0], v.params[0], v.params[1] / 2.0]), np.asarray(v.xyz, dtype=float)
+        elif v.kind == "sphere":
+            semi, center = np.array([v.params[0]] * 3), np.asarray(v.xyz, dtype=float)
+        else:
+            fn = v.filename
+            path = os.path.join(root, fn[len("package://"):]) if fn.startswith("package://") else \
+                os.path.join(os.path.dirname(os.path.abspath(urdf_file)), fn)
+            if not os.path.exists(path):
+                out.append(None)
+                continue
+            lo, hi = mesh_aabb(path)
+            semi, center = (hi - lo) / 2.0, (hi + lo) / 2.0 + np.asarray(v.xyz, dtype=float)
+        out.append({"link": v.link, "semi_axes": semi, "center": center})
     return out
 
 
@@ -453,6 +518,7 @@ def build_model_from_urdf(urdf_file: str, config_file: str | None = None,
         model.link_names = list(rc.get("link_names", []) or [])
         for n in model.end_effector_names:
             model.frame_id(n)  # raises like pinocchio's getFrameId on an unknown name
+        model.bounding_ellipsoids = bounding_ellipsoids(model, urdf_file)
     return model
 
 

@@ -1,0 +1,182 @@
+"""``Solver`` — drop-in for src/solver.py:5, plus the Gram-compressed input.
+
+The reference hands CVXPY the stacked N·nv x W matrices (solver.py:186-190).  The engine produces the
+normal equations instead (G = AᵀA, g = Aᵀb, bᵀb, num_rows), so this Solver accepts either form:
+
+    Solver(Y_proj, tau_proj, num_links, phi_prior, total_mass, ellipsoids, B_v=..., B_c=...)   # reference
+    Solver.from_normal_equations(ne, num_links, phi_prior, total_mass, ellipsoids, friction=True)
+
+With the Gram, ``sum_squares(A x - b)`` becomes ``sum_squares(R x) - 2 gᵀx + bᵀb`` (R = chol(G)ᵀ), so CVXPY
+sees W rows instead of N·nv and the 1/(N·nv) scale of solver.py:190 is kept via ``num_rows``.
+
+``solve_llsq_svd`` (solver.py:32-39) is plain numpy.  ``solve_fully_consistent`` (:123-210) needs cvxpy and
+the MOSEK licence exactly like the reference; neither is installed in this project's images, so it raises
+ImportError there (φ parity is unverifiable without them — SURVEY.md §8c).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+class Solver():
+    def __init__(self, regressor, tau_vec, num_links, phi_prior, total_mass, bounding_ellipsoids, B_v=None, B_c=None,
+                 *, normal_equations=None):
+        if normal_equations is None:
+            self._Y = np.asarray(regressor)
+            self._tau = np.asarray(tau_vec)
+            self._nx = self._Y.shape[1]
+            self._num_samples = self._Y.shape[0]          # rows = N·nv, the objective's divisor
+            self._gram = None
+        else:
+            ne = normal_equations
+            self._Y = None
+            self._tau = None
+            self._gram = ne
+            self._nx = int(ne["nx"])
+            self._num_samples = int(ne["num_rows"])
+        self._num_links = num_links
+        self._num_inertial_params = self._nx // self._num_links
+        self._phi_prior = phi_prior
+        self.total_mass = total_mass
+        self._bounding_ellipsoids = bounding_ellipsoids
+        self._identify_fric = (B_v is not None and B_c is not None) or (
+            normal_equations is not None and normal_equations.get("ndof", 0) > 0)
+        if self._identify_fric:
+            self._B_v, self._B_c = B_v, B_c
+            self.ndof = B_v.shape[1] if B_v is not None else int(normal_equations["ndof"])
+        self._objective = None
+        self._constraints = []
+        self._problem = None
+
+    @classmethod
+    def from_normal_equations(cls, ne: dict, num_links, phi_prior, total_mass, bounding_ellipsoids,
+                              friction: bool = True, ndof: int | None = None):
+        """``ne`` as returned by SystemIdentification.build_normal_equations (gram is W x W with
+        W = 10·num_links + 2·ndof when friction columns are present)."""
+        W = ne["gram"].shape[0]
+        nphi = 10 * num_links
+        nd = (W - nphi) // 2 if friction else 0
+        if ndof is not None and friction and ndof != nd:
+            raise ValueError("ndof does not match the Gram size")
+        d = dict(ne)
+        d["nx"] = nphi
+        d["ndof"] = nd
+        d["W"] = W
+        return cls(None, None, num_links, phi_prior, total_mass, bounding_ellipsoids, normal_equations=d)
+
+    # -------------- Unconstrained Solver -------------- #
+    def solve_llsq_svd(self):
+        """solver.py:32-39: minimum-norm least squares of Y phi = tau (friction columns not used)."""
+        if self._gram is None:
+            U, Sigma, VT = np.linalg.svd(self._Y, full_matrices=False)
+            Sigma_inv = np.linalg.pinv(np.diag(Sigma))
+            return VT.T @ Sigma_inv @ U.T @ self._tau
+        # same minimum-norm solution from the normal equations: x = pinv(G_YY) g_Y
+        n = self._nx
+        G = self._gram["gram"][:n, :n]
+        g = self._gram["Atb"][:n]
+        w, V = np.linalg.eigh(G)
+        # singular values of Y are sqrt(w); keep the numpy pinv cut (1e-15 sigma_max) on sigma
+        sig = np.sqrt(np.clip(w, 0.0, None))
+        keep = sig > 1e-15 * sig.max()
+        return V[:, keep] @ ((V[:, keep].T @ g) / w[keep])
+
+    # ------------ Constrained Solver (LMI) ------------ #
+    def solve_fully_consistent(self, lambda_reg=1e-1, tol=1e-10, max_iters=1000, reg_type="constant_pullback"):
+        try:
+            import cvxpy as cp  # noqa: F401
+        except ImportError as exc:  # pragma: no cover - depends on the host image
+            raise ImportError("solve_fully_consistent needs cvxpy and MOSEK (src/solver.py:2,195), which are not "
+                              "installed; use solve_llsq_svd or install them on the solving host") from exc
+        return _solve_fully_consistent_cvxpy(self, lambda_reg, tol, max_iters, reg_type)
+
+
+def _pseudo_inertia(phi):
+    mass, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = phi
+    tr = 0.5 * (Ixx + Iyy + Izz)
+    return np.array([[tr - Ixx, -Ixy, -Ixz, hx], [-Ixy, tr - Iyy, -Iyz, hy], [-Ixz, -Iyz, tr - Izz, hz],
+                     [hx, hy, hz, mass]])
+
+
+def pullback_metric(phi_prior_link):
+    """solver.py:95-121 — constant pull-back approximation of the Riemannian metric at the prior."""
+    M = np.zeros((10, 10))
+    P_inv = np.linalg.inv(_pseudo_inertia(phi_prior_link))
+    for i in range(10):
+        for j in range(10):
+            vi = np.zeros(10)
+            vj = np.zeros(10)
+            vi[i] = 1
+            vj[j] = 1
+            M[i, j] = np.trace(P_inv @ _pseudo_inertia(vi) @ P_inv @ _pseudo_inertia(vj))
+    M = (M + M.T) / 2
+    ev = np.linalg.eigvals(M)
+    if np.any(ev < 0):
+        M = M + (-np.min(ev) + 1e-5) * np.eye(10)
+    assert np.min(np.linalg.eigvals(M)) > 0
+    return M
+
+
+def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_type):  # pragma: no cover
+    import cvxpy as cp
+    nx = s._nx
+    phi = cp.Variable(nx, value=np.asarray(s._phi_prior, dtype=float))
+    cons = []
+    reg = 0
+    mass_sum = 0
+    for idx in range(s._num_links):
+        j = idx * 10
+        p = phi[j:j + 10]
+        prior = np.asarray(s._phi_prior[j:j + 10], dtype=float)
+        ell = s._bounding_ellipsoids[idx]
+        semi, center = np.asarray(ell["semi_axes"]), np.asarray(ell["center"])
+        cons.append(p[0] >= 0)
+        mass_sum += p[0]
+        m, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = [p[k] for k in range(10)]
+        tr = 0.5 * (Ixx + Iyy + Izz)
+        J = cp.vstack([cp.hstack([tr - Ixx, -Ixy, -Ixz, hx]), cp.hstack([-Ixy, tr - Iyy, -Iyz, hy]),
+                       cp.hstack([-Ixz, -Iyz, tr - Izz, hz]), cp.hstack([hx, hy, hz, m])])
+        cons.append(J + 1e-6 * np.eye(4) >> 0)
+        Qs = np.diag(semi) ** 2
+        tr_ = cp.reshape(p[1:4] - p[0] * center, (1, 3))
+        com = cp.bmat([[cp.reshape(p[0], (1, 1)), tr_], [tr_.T, p[0] * Qs]])
+        cons.append(com + 1e-6 * np.eye(4) >> 0)
+        Q = np.linalg.inv(np.diag(semi) ** 2)
+        Qf = np.zeros((4, 4))
+        Qf[:3, :3] = Q
+        Qf[:3, 3] = Q @ center
+        Qf[3, :3] = Q @ center
+        Qf[3, 3] = 1 - center @ Q @ center
+        cons.append(cp.trace(J @ Qf) >= 0)
+        if reg_type == "constant_pullback":
+            reg += 0.5 * cp.quad_form(p - prior, pullback_metric(prior))
+    if reg_type == "euclidean":
+        reg = cp.quad_form(phi - np.asarray(s._phi_prior, dtype=float), np.eye(nx))
+    cons.append(mass_sum == s.total_mass)
+    if s._gram is None:
+        if s._identify_fric:
+            bv, bc = cp.Variable(s.ndof), cp.Variable(s.ndof)
+            cons += [bv >= 0, bc >= 0]
+            err = cp.sum_squares(s._Y @ phi + s._B_v @ bv + s._B_c @ bc - s._tau)
+        else:
+            err = cp.sum_squares(s._Y @ phi - s._tau)
+    else:
+        G, g, btb = s._gram["gram"], s._gram["Atb"], s._gram["btb"]
+        if s._identify_fric:
+            bv, bc = cp.Variable(s.ndof), cp.Variable(s.ndof)
+            cons += [bv >= 0, bc >= 0]
+            x = cp.hstack([phi, bv, bc])
+        else:
+            x = phi
+            G, g = G[:nx, :nx], g[:nx]
+        w, V = np.linalg.eigh(G)
+        R = (V * np.sqrt(np.clip(w, 0, None))).T
+        err = cp.sum_squares(R @ x) - 2 * g @ x + btb
+    prob = cp.Problem(cp.Minimize(0.5 * err / s._num_samples + lambda_reg * reg), cons)
+    prob.solve(solver=cp.MOSEK, mosek_params={"MSK_IPAR_INTPNT_SOLVE_FORM": "MSK_SOLVE_PRIMAL",
+                                              "MSK_DPAR_INTPNT_TOL_REL_GAP": tol,
+                                              "MSK_DPAR_OPTIMIZER_MAX_TIME": 100.0,
+                                              "MSK_IPAR_INTPNT_MAX_ITERATIONS": max_iters}, verbose=True)
+    if prob.status in (cp.OPTIMAL, cp.OPTIMAL_INACCURATE):
+        return phi.value
+    raise ValueError("The problem did not solve to optimality.")

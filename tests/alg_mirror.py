@@ -2,7 +2,7 @@
 
 The kernel does not follow pinocchio's backward pass.  It uses, per sample:
 
-* world motion axes of every dof: ``w_r`` (direction) and ``p_r`` (point on the axis);
+* motion axes of every dof in the base (free-flyer) frame: ``w_r`` (direction) and ``p_r`` (a point);
 * the contact Jacobian from the same axes; ``P = I - Q^T Q`` with ``Q = L^-1 J_c``, ``L L^T = J_c J_c^T``;
 * ``H_i = P · M_i · J_w^T`` (nv x 6, world coordinates), built by one rank-1 update per body from its
   parent (``M_i`` = mask of the dofs supporting body i);
@@ -70,9 +70,21 @@ def projector_cholqr(model, d, cnt, W, Pt, lin, tol=1e-12):
     return np.eye(nv) - Q.T @ Q
 
 
+def base_relative(model, d):
+    """Poses relative to the free-flyer frame (the kernel's reference frame); v, a_gf unchanged."""
+    for i in range(1, model.njoints):
+        p = model.parents[i]
+        if model.jtypes[i] == JOINT_FREEFLYER:
+            d.oR[i], d.ot[i] = np.eye(3), np.zeros(3)
+        else:
+            d.oR[i] = d.oR[p] @ d.liR[i]
+            d.ot[i] = d.oR[p] @ d.lit[i] + d.ot[p]
+    return d
+
+
 def sample_panel(model, q, dq, ddq, tau, cnt):
     """[Y_proj | B_v | B_c | tau_proj] for one sample via the kernel formulation."""
-    d = ref.forward_pass(model, q, dq, ddq)
+    d = base_relative(model, ref.forward_pass(model, q, dq, ddq))
     W, Pt, lin = world_axes(model, d)
     P = projector_cholqr(model, d, cnt, W, Pt, lin)
     nv, nb = model.nv, model.nb

@@ -1,0 +1,124 @@
+"""URDF -> model compiler (needs the reference checkout for the URDFs; the committed JSON elsewhere)."""
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+from oracle import ref_numpy as ref
+from system_identification_amd.model import (Model, build_model_from_urdf, load_robot, rpy_to_matrix, ROBOTS,
+                                             JOINT_FREEFLYER)
+from tests.conftest import REFERENCE, needs_reference
+
+SOURCES = {
+    "solo12": ("files/solo_description/solo12.urdf", "files/solo_description/solo12_config.yaml"),
+    "spot": ("files/spot_description/spot.urdf", "files/spot_description/spot_config.yaml"),
+}
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_committed_dims(robot):
+    m = load_robot(robot)
+    expect = {"solo12": (19, 18, 13, 4), "spot": (19, 18, 13, 4), "g1_29dof": (36, 35, 30, 2)}[robot]
+    assert (m.nq, m.nv, m.nb, m.n_ee) == expect
+    assert m.jtypes[1] == JOINT_FREEFLYER and m.parents[1] == 0
+    # DFS numbering: a parent always precedes its children
+    assert all(m.parents[i] < i for i in range(1, m.njoints))
+
+
+@needs_reference
+@pytest.mark.parametrize("robot", list(SOURCES))
+def test_committed_json_is_fresh(robot):
+    u, c = SOURCES[robot]
+    fresh = build_model_from_urdf(os.path.join(REFERENCE, u), os.path.join(REFERENCE, c))
+    assert fresh.to_json() == load_robot(robot).to_json()
+
+
+def _urdf_link_poses(urdf, joint_values):
+    """Independent walk of the URDF: world pose of every link for given joint angles (root at identity)."""
+    root = ET.parse(urdf).getroot()
+    joints = root.findall("joint")
+    child = {j.find("child").get("link"): j for j in joints}
+    poses = {}
+
+    def pose(link):
+        if link in poses:
+            return poses[link]
+        if link not in child:
+            poses[link] = (np.eye(3), np.zeros(3))
+            return poses[link]
+        j = child[link]
+        Rp, tp = pose(j.find("parent").get("link"))
+        o = j.find("origin")
+        xyz = np.array([float(x) for x in o.get("xyz", "0 0 0").split()]) if o is not None else np.zeros(3)
+        rpy = np.array([float(x) for x in o.get("rpy", "0 0 0").split()]) if o is not None else np.zeros(3)
+        R = Rp @ rpy_to_matrix(*rpy)
+        t = Rp @ xyz + tp
+        if j.get("type") == "revolute":
+            ax = np.array([float(x) for x in j.find("axis").get("xyz").split()])
+            th = joint_values[j.get("name")]
+            K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+            R = R @ (np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K)
+        poses[link] = (R, t)
+        return poses[link]
+
+    for l in root.findall("link"):
+        pose(l.get("name"))
+    return poses
+
+
+@needs_reference
+@pytest.mark.parametrize("robot", list(SOURCES) + ["g1_29dof"])
+def test_frames_match_independent_urdf_walk(robot):
+    m = load_robot(robot)
+    urdf = os.path.join(REFERENCE, SOURCES[robot][0]) if robot in SOURCES else \
+        os.path.join(REFERENCE, "files/g1_description/g1_29dof.urdf")
+    rng = np.random.default_rng(0)
+    q = np.zeros(m.nq)
+    q[6] = 1.0  # identity base
+    vals = {}
+    for i in range(2, m.njoints):
+        q[m.idx_q[i]] = rng.uniform(-1, 1)
+        vals[m.joint_names[i]] = q[m.idx_q[i]]
+    d = ref.forward_pass(m, q, np.zeros(m.nv), np.zeros(m.nv))
+    poses = _urdf_link_poses(urdf, vals)
+    for f in m.frames:
+        if f.kind != "body":
+            continue
+        R = d.oR[f.parent] @ f.R
+        t = d.oR[f.parent] @ f.t + d.ot[f.parent]
+        Rr, tr = poses[f.name]
+        assert np.allclose(R, Rr, atol=1e-12) and np.allclose(t, tr, atol=1e-12), f.name
+
+
+def test_children_are_visited_in_joint_name_order(tmp_path):
+    urdf = """<robot name="t"><link name="b"/><link name="x"/><link name="y"/>
+      <joint name="zz" type="revolute"><parent link="b"/><child link="x"/><axis xyz="0 0 1"/></joint>
+      <joint name="aa" type="revolute"><parent link="b"/><child link="y"/><axis xyz="1 0 0"/></joint></robot>"""
+    p = tmp_path / "t.urdf"
+    p.write_text(urdf)
+    m = build_model_from_urdf(str(p), None, floating_base=True)
+    assert m.joint_names == ["universe", "root_joint", "aa", "zz"]
+
+
+def test_unsupported_joint_raises(tmp_path):
+    urdf = """<robot name="t"><link name="b"/><link name="x"/>
+      <joint name="p" type="prismatic"><parent link="b"/><child link="x"/><axis xyz="0 0 1"/></joint></robot>"""
+    p = tmp_path / "t.urdf"
+    p.write_text(urdf)
+    with pytest.raises(NotImplementedError):
+        build_model_from_urdf(str(p), None)
+
+
+def test_fixed_joint_inertia_is_merged():
+    """Spot: pinocchio body 1 = URDF body + base_link + rails."""
+    m = load_robot("spot")
+    assert abs(m.inertias[1].mass - (16.52 + 2e-6)) < 1e-9
+
+
+def test_json_round_trip(tmp_path):
+    m = load_robot("solo12")
+    p = tmp_path / "m.json"
+    m.save_json(str(p))
+    m2 = Model.load_json(str(p))
+    assert m2.to_json() == m.to_json() and m2.pack() == m.pack()
