@@ -44,7 +44,7 @@ struct sysid_engine {
   int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4;
   size_t k1_lds = 0;
   // K2/K3 Gram tiling
-  int ntc = 0, nslots = 0, ngroups = 0, stride = 0, kc = 0;
+  int ntc = 0, nslots = 0, nsuper = 0, ngroups = 0;
   int2* d_tiles = nullptr;
   // host-API buffers (grow-only)
   double* d_in = nullptr;
@@ -80,7 +80,7 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 
 int ksplit_for(const sysid_engine* e, int64_t rows) {
   int ks = std::max(1, e->cus / std::max(1, e->ngroups));
-  const int64_t cap = std::max<int64_t>(1, (rows + 4 * e->kc - 1) / (4 * e->kc));  // >= 4 chunks each
+  const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
 }
 
@@ -142,17 +142,33 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
       return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, sb + pb);
     double* slab = static_cast<double*>(d_ws);
     double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + sb);
-    const size_t lds2 = (size_t)2 * e->kc * e->stride * sizeof(double);
-    hipLaunchKernelGGL(k2_gram_syrk, dim3(e->ngroups * ks), dim3(64 * K2_WAVES), lds2, st, d_panel, rows, ld_panel,
-                       e->ncol, e->ntc, e->stride, e->kc, e->d_tiles, e->ngroups, ks, e->nslots, slab);
+    if (ld_panel > 16 * e->ntc)
+      return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
+    const dim3 g2(e->ngroups * ks), b2(64 * K2_WAVES);
+    switch (e->ntc) {
+#define SYSID_K2_CASE(NTC, KC)                                                                               \
+  case NTC:                                                                                                 \
+    hipLaunchKernelGGL((k2_gram_syrk<NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles, e->ngroups,  \
+                       ks, e->nslots, slab);                                                                \
+    break;
+      SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
+      SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
+      SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20)
+      SYSID_K2_CASE(15, 20) SYSID_K2_CASE(16, 16) SYSID_K2_CASE(17, 16) SYSID_K2_CASE(18, 16)
+      SYSID_K2_CASE(19, 16) SYSID_K2_CASE(20, 16) SYSID_K2_CASE(21, 12) SYSID_K2_CASE(22, 12)
+      SYSID_K2_CASE(23, 12) SYSID_K2_CASE(24, 12)
+#undef SYSID_K2_CASE
+      default:
+        return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
+    }
     HIP_TRY(e, hipGetLastError());
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
     const int64_t nx = (int64_t)e->nslots * 256;
     hipLaunchKernelGGL(k3_gram_partial, dim3((unsigned)((nx + 255) / 256), rs), dim3(256), 0, st, slab, nx, ks, rs,
                        part);
     HIP_TRY(e, hipGetLastError());
-    hipLaunchKernelGGL(k3_gram_final, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, part, e->d_tiles,
-                       e->nslots, rs, e->ncol, d_gram);
+    hipLaunchKernelGGL(k3_gram_final, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, part,
+                       e->d_tiles + e->nsuper, e->nslots, rs, e->ncol, d_gram);
     HIP_TRY(e, hipGetLastError());
     if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
   } else if (ev) {
@@ -216,6 +232,9 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   }
   if (qcount != nq || vcount != nv)
     return set_err(nullptr, SYSID_E_MODEL, "joint dims do not add up (nq %d/%d, nv %d/%d)", qcount, nq, vcount, nv);
+  if (10 * (NJ - 1) + 2 * nja + 1 > 384)
+    return set_err(nullptr, SYSID_E_MODEL, "regressor too wide for the Gram kernels (W+1 = %d > 384)",
+                   10 * (NJ - 1) + 2 * nja + 1);
   if (nff > 1) return set_err(nullptr, SYSID_E_MODEL, "at most one free-flyer (the root) is supported");
   if (bd == 6 && !(nff == 1 && ff0 == 0))
     return set_err(nullptr, SYSID_E_MODEL, "floating base requires the free-flyer as the first joint");
@@ -286,18 +305,29 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;
 
-  // Gram tiling: upper-triangular 16x16 tiles, groups of K2_WAVES x K2_TPW slots
+  // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
+  // K2_WAVES x K2_SPW super slots per workgroup group; 4 tile slots per super slot.
   e->ntc = (e->ncol + 15) / 16;
-  std::vector<int2> tl;
-  for (int I0 = 0; I0 < e->ntc; ++I0)
-    for (int J0 = I0; J0 < e->ntc; ++J0) tl.push_back(int2{I0, J0});
-  const int per_group = K2_WAVES * K2_TPW;
-  e->ngroups = ((int)tl.size() + per_group - 1) / per_group;
-  tl.resize((size_t)e->ngroups * per_group, int2{-1, -1});
+  const int nsg = (e->ntc + 1) / 2;
+  std::vector<int2> sl;
+  for (int I0 = 0; I0 < nsg; ++I0)
+    for (int J0 = I0; J0 < nsg; ++J0) sl.push_back(int2{I0, J0});
+  const int per_group = K2_WAVES * K2_SPW;
+  e->ngroups = ((int)sl.size() + per_group - 1) / per_group;
+  sl.resize((size_t)e->ngroups * per_group, int2{-1, -1});
+  std::vector<int2> tl(sl.size() * 4, int2{-1, -1});
+  for (size_t k = 0; k < sl.size(); ++k) {
+    if (sl[k].x < 0) continue;
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) {
+        const int I0 = 2 * sl[k].x + a, J0 = 2 * sl[k].y + b;
+        if (I0 <= J0 && I0 < e->ntc && J0 < e->ntc) tl[4 * k + 2 * a + b] = int2{I0, J0};
+      }
+  }
   e->nslots = (int)tl.size();
-  e->stride = ((e->ntc * 16 + 31) / 32) * 32 + 16;  // conflict-free ds_read_b64 of 2 rows x 16 doubles
-  e->kc = std::max(4, ((64 * K2_WAVES * K2_PER) / (e->ntc * 8)) / 4 * 4);
-  while (e->kc > 4 && (size_t)2 * e->kc * e->stride * 8 > 150 * 1024) e->kc -= 4;
+  std::vector<int2> both(sl);
+  both.insert(both.end(), tl.begin(), tl.end());  // d_tiles = [super slots | tile slots]
+  e->nsuper = (int)sl.size();
 
   hipError_t st = hipSetDevice(device);
   hipDeviceProp_t prop;
@@ -306,8 +336,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-  if (st == hipSuccess) st = hipMalloc(&e->d_tiles, tl.size() * sizeof(int2));
-  if (st == hipSuccess) st = hipMemcpy(e->d_tiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMalloc(&e->d_tiles, both.size() * sizeof(int2));
+  if (st == hipSuccess) st = hipMemcpy(e->d_tiles, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice);
   // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget
   if (st == hipSuccess) {
     int best = -1;
@@ -326,9 +356,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     }
     st = hipFuncSetAttribute(k1_fn(maxch_tpl), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
   }
-  if (st == hipSuccess)
-    st = hipFuncSetAttribute(reinterpret_cast<const void*>(k2_gram_syrk), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)((size_t)2 * e->kc * e->stride * sizeof(double)));
   if (st != hipSuccess) {
     set_err(nullptr, SYSID_E_DEVICE, "device setup failed: %s", hipGetErrorString(st));
     sysid_destroy(e);

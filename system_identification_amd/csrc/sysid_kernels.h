@@ -20,8 +20,6 @@ constexpr int JT_FREEFLYER = 1;
 constexpr int JT_REVOLUTE = 2;
 constexpr int K1_WAVES = 4;            // waves (= samples in flight) per K1 workgroup
 constexpr int K2_WAVES = 8;            // waves per K2 workgroup
-constexpr int K2_TPW = 7;              // Gram tiles per K2 wave (8 x 7 = 56 slots per group)
-constexpr int K2_PER = 8;              // max staged double2 per thread per chunk
 
 // ------------------------------------------------------------------------------------------------
 // layouts shared by host and device
@@ -228,7 +226,10 @@ __device__ __forceinline__ void wsync() {
 // K1
 // ------------------------------------------------------------------------------------------------
 template <int MAXCH>
-__global__ void __launch_bounds__(64 * K1_WAVES)
+#ifndef SYSID_K1_MIN_WAVES_PER_EU
+#define SYSID_K1_MIN_WAVES_PER_EU 1
+#endif
+__global__ void __launch_bounds__(64 * K1_WAVES, SYSID_K1_MIN_WAVES_PER_EU)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
                    int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp, double* __restrict__ dbg) {
   extern __shared__ double smem[];
@@ -566,91 +567,126 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 
 // ------------------------------------------------------------------------------------------------
 // K2: G_partial[ks] = panel[rows of ks]^T panel[rows of ks]   (fp64 MFMA 16x16x4, upper tiles)
+//
+// Each workgroup (K2_WAVES waves) walks a contiguous row range in chunks of KC rows.  A chunk of the
+// panel is one contiguous byte range in HBM; every thread copies fixed double2 slots of it (offsets
+// computed once, no divisions in the loop) through registers into an LDS buffer with a padded row
+// stride (STRIDE ≡ 16 mod 32 doubles, so the 2 rows x 16 doubles of a 32-lane ds_read_b64 group hit
+// disjoint banks).  Two LDS buffers: chunk c+1's global loads are in flight while chunk c is multiplied.
+// Each wave owns K2_SPW "super-tiles" (2x2 blocks of 16x16 output tiles): 4 fragment reads feed 4 MFMAs.
+// The k-loop over a chunk is fully unrolled, so fragment reads use immediate LDS offsets.
+// Fragment = 16 consecutive doubles of 4 consecutive rows: lane l holds row (l>>4), col (l&15), which is
+// both the A layout (A[i=l&15][k=l>>4]) and the B layout (B[k=l>>4][j=l&15]) of v_mfma_f64_16x16x4_f64.
 // ------------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int K2_SPW = 2;   // super-tiles per wave
 
+__host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) / 32) * 32 + 16; }
+
+template <int NTC, int KC>
 __global__ void __launch_bounds__(64 * K2_WAVES)
-k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, int ncol, int ntc, int stride,
-             int kc, const int2* __restrict__ tiles, int ngroups, int ksplit, int nslots,
-             double* __restrict__ slab) {
-  extern __shared__ double buf[];  // 2 x kc x stride
+k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+             int ngroups, int ksplit, int nslots, double* __restrict__ slab) {
+  constexpr int STRIDE = k2_stride(NTC);
+  constexpr int BUF = KC * STRIDE;                       // doubles per LDS buffer
+  constexpr int NT = 64 * K2_WAVES;
+  __shared__ double lds[2 * BUF];
   const int group = blockIdx.x % ngroups;
   const int ks = blockIdx.x / ngroups;
-  const int64_t r0 = rows * ks / ksplit, r1 = rows * (ks + 1) / ksplit;
+  const int64_t q4 = rows / 4;
+  const int64_t r0 = 4 * (q4 * ks / ksplit);
+  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int slot0 = (group * K2_WAVES + wave) * K2_TPW;
-  int tI[K2_TPW], tJ[K2_TPW];
-#pragma unroll
-  for (int t = 0; t < K2_TPW; ++t) {
-    const int2 ij = tiles[slot0 + t];
-    tI[t] = ij.x;
-    tJ[t] = ij.y;
-  }
-  dbl4 acc[K2_TPW];
-#pragma unroll
-  for (int t = 0; t < K2_TPW; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const int sbase = (group * K2_WAVES + wave) * K2_SPW;
 
-  const int half = ntc * 8;  // double2 per staged row
-  const int pairs = kc * half;
-  double2 st[K2_PER];
-  auto load_chunk = [&](int64_t c0) {
+  // zero both buffers once: columns >= ldp (up to NTC*16) are never staged and must read as 0
+  for (int x = threadIdx.x; x < 2 * BUF; x += NT) lds[x] = 0.0;
+
+  // staging slots: the chunk is KC*ldp contiguous doubles; thread slot u copies doubles [2x, 2x+1]
+  const int chunk_d2 = (int)((KC * ldp) / 2);            // ldp is even
+  constexpr int PER = (KC * NTC * 8 + NT - 1) / NT;       // >= ceil(KC*ldp/2 / NT)
+  int loff[PER];
+  bool used[PER];
 #pragma unroll
-    for (int u = 0; u < K2_PER; ++u) {
-      const int e = threadIdx.x + u * 64 * K2_WAVES;
-      double2 v = {0.0, 0.0};
-      if (e < pairs) {
-        const int rr = e / half, col = 2 * (e - rr * half);
-        const int64_t g = c0 + rr;
-        if (g < r1 && col < ncol) {
-          v = *reinterpret_cast<const double2*>(panel + g * ldp + col);
-          if (col + 1 >= ncol) v.y = 0.0;
-        }
-      }
-      st[u] = v;
+  for (int u = 0; u < PER; ++u) {
+    const int x = threadIdx.x + u * NT;
+    used[u] = x < chunk_d2;
+    const int e = 2 * x;
+    const int row = used[u] ? e / (int)ldp : 0;
+    loff[u] = used[u] ? row * STRIDE + (e - row * (int)ldp) : 0;
+  }
+  double2 st[PER];
+  auto load_chunk = [&](int64_t c0) {
+    const double2* src = reinterpret_cast<const double2*>(panel + c0 * ldp);
+    const int64_t lim = (r1 - c0) * ldp / 2;  // double2 slots inside [c0, r1)
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int x = threadIdx.x + u * NT;
+      st[u] = (used[u] && x < lim) ? src[x] : double2{0.0, 0.0};
     }
   };
   auto store_chunk = [&](double* b) {
 #pragma unroll
-    for (int u = 0; u < K2_PER; ++u) {
-      const int e = threadIdx.x + u * 64 * K2_WAVES;
-      if (e < pairs) {
-        const int rr = e / half, col = 2 * (e - rr * half);
-        *reinterpret_cast<double2*>(b + rr * stride + col) = st[u];
-      }
-    }
+    for (int u = 0; u < PER; ++u)
+      if (used[u]) *reinterpret_cast<double2*>(b + loff[u]) = st[u];
   };
-  const int64_t nchunks = (r1 - r0 + kc - 1) / kc;
-  const int kr = lane >> 4, k16 = lane & 15;
+
+  // fragment columns of this wave: f = 4*s + {I0, I0+1, J0, J0+1} (16-column blocks)
+  int foff[4 * K2_SPW];
+  bool live[K2_SPW];
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s) {
+    const int2 sp = supers[sbase + s];
+    live[s] = sp.x >= 0;
+    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
+      foff[4 * s + u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
+    }
+  }
+  dbl4 acc[K2_SPW][4];
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[s][t] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  const int64_t nchunks = (r1 - r0 + KC - 1) / KC;
+  __syncthreads();  // LDS zeroed
   if (nchunks > 0) {
     load_chunk(r0);
-    store_chunk(buf);
+    store_chunk(lds);
   }
   __syncthreads();
   for (int64_t c = 0; c < nchunks; ++c) {
-    double* cur = buf + (c & 1) * kc * stride;
-    double* nxt = buf + ((c + 1) & 1) * kc * stride;
-    if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * kc);
-    for (int kk = 0; kk < kc; kk += 4) {
-      const double* rowp = cur + (kk + kr) * stride + k16;
-      double a[K2_TPW], b[K2_TPW];
+    const double* cur = lds + (c & 1) * BUF;
+    if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * KC);
 #pragma unroll
-      for (int t = 0; t < K2_TPW; ++t) {
-        a[t] = tI[t] >= 0 ? rowp[tI[t] * 16] : 0.0;
-        b[t] = tI[t] >= 0 ? rowp[tJ[t] * 16] : 0.0;
+    for (int kk = 0; kk < KC; kk += 4) {
+      double x[4 * K2_SPW];
+#pragma unroll
+      for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = cur[foff[u] + kk * STRIDE];
+#pragma unroll
+      for (int s = 0; s < K2_SPW; ++s) {
+        acc[s][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 2], acc[s][0], 0, 0, 0);
+        acc[s][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 3], acc[s][1], 0, 0, 0);
+        acc[s][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 2], acc[s][2], 0, 0, 0);
+        acc[s][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 3], acc[s][3], 0, 0, 0);
       }
-#pragma unroll
-      for (int t = 0; t < K2_TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc[t], 0, 0, 0);
     }
-    if (c + 1 < nchunks) store_chunk(nxt);
+    if (c + 1 < nchunks) store_chunk(lds + ((c + 1) & 1) * BUF);
     __syncthreads();
   }
   // D layout of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
-  for (int t = 0; t < K2_TPW; ++t) {
-    if (tI[t] < 0) continue;
-    double* o = slab + ((size_t)ks * nslots + slot0 + t) * 256;
+  for (int s = 0; s < K2_SPW; ++s) {
+    if (!live[s]) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[((lane >> 4) + 4 * j) * 16 + (lane & 15)] = acc[t][j];
+    for (int t = 0; t < 4; ++t) {
+      double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[((lane >> 4) + 4 * j) * 16 + (lane & 15)] = acc[s][t][j];
+    }
   }
 }
 

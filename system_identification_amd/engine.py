@@ -27,7 +27,7 @@ EMIT_GRAM = 8
 EMIT_ALL = 15
 
 LIB_NAME = "libsysid.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("SYSID_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 # (name, restype, argtypes) — one entry per function declared in include/sysid.h
 _c = ctypes
