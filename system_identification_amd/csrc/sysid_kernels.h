@@ -448,6 +448,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     for (int e = lane; e < k * k; e += 64) {
       const int a = e / k, b = e - a * k;
       double acc = 0.0;
+#pragma unroll 6
       for (int r = 0; r < nv; ++r) acc += Jc[a * nv + r] * Jc[b * nv + r];
       Ms[e] = acc;
     }
@@ -482,6 +483,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       for (int j = 0; j < k; ++j) {
         const double ljj = Ms[j * k + j];
         double x = Jc[j * nv + r];
+#pragma unroll 4
         for (int l = 0; l < j; ++l) x -= Ms[j * k + l] * Jc[l * nv + r];
         Jc[j * nv + r] = ljj != 0.0 ? x / ljj : 0.0;
       }
@@ -492,6 +494,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     for (int e = lane; e < nv * nv; e += 64) {
       const int a = e / nv, b = e - a * nv;
       double acc = 0.0;
+#pragma unroll 4
       for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Jc[j * nv + b];
       Ps[e] = (a == b ? 1.0 : 0.0) - acc;
     }
@@ -509,6 +512,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       } else {
         const int r = e - nv * 6;
         double acc = 0.0;
+#pragma unroll 4
         for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
         tps[r] = acc;
       }
@@ -530,24 +534,53 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         body_regressor_world_column(body + 24 * i, p, fw);
         // revolute ancestors of body i (and i): c_t = J_w[:, dof_t] . fw
         const int cl = chain_len[i];
-        int dof[MAXCH];
-        double cv[MAXCH];
+        if constexpr (MAXCH <= 8) {
+          // short chains: unused slots read a valid P column with a zero coefficient, so the row
+          // loop has no branch and all of its LDS reads are in flight together
+          int pofs[MAXCH];
+          double cv[MAXCH];
 #pragma unroll
-        for (int t = 0; t < MAXCH; ++t) {
-          dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
-          const double* jw = Jws + 6 * dof[t];
-          cv[t] = t < cl ? jw[0] * fw[0] + jw[1] * fw[1] + jw[2] * fw[2] + jw[3] * fw[3] + jw[4] * fw[4] +
-                               jw[5] * fw[5]
-                         : 0.0;
-        }
-        for (int r = 0; r < nv; ++r) {
-          const double* h = H1 + 6 * r;
-          double acc = h[0] * fw[0] + h[1] * fw[1] + h[2] * fw[2] + h[3] * fw[3] + h[4] * fw[4] + h[5] * fw[5];
-          const double* pr = Ps + r * nv;
+          for (int t = 0; t < MAXCH; ++t) {
+            const int d = t < cl ? chain[i * kp.maxch + t] : 0;
+            const double* jw = Jws + 6 * d;
+            const double c = jw[0] * fw[0] + jw[1] * fw[1] + jw[2] * fw[2] + jw[3] * fw[3] + jw[4] * fw[4] +
+                             jw[5] * fw[5];
+            cv[t] = t < cl ? c : 0.0;
+            pofs[t] = d;
+          }
+#pragma unroll 2
+          for (int r = 0; r < nv; ++r) {
+            const double* h = H1 + 6 * r;
+            const double* pr = Ps + r * nv;
+            double pv[MAXCH];
 #pragma unroll
-          for (int t = 0; t < MAXCH; ++t)
-            if (t < cl) acc += pr[dof[t]] * cv[t];
-          out[(int64_t)r * ldp + col] = acc;
+            for (int t = 0; t < MAXCH; ++t) pv[t] = pr[pofs[t]];
+            double acc = h[0] * fw[0] + h[1] * fw[1] + h[2] * fw[2] + h[3] * fw[3] + h[4] * fw[4] + h[5] * fw[5];
+#pragma unroll
+            for (int t = 0; t < MAXCH; ++t) acc += pv[t] * cv[t];
+            out[(int64_t)r * ldp + col] = acc;
+          }
+        } else {
+          // long chains (humanoids): predicated terms keep the register footprint bounded
+          int dof[MAXCH];
+          double cv[MAXCH];
+#pragma unroll
+          for (int t = 0; t < MAXCH; ++t) {
+            dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
+            const double* jw = Jws + 6 * dof[t];
+            cv[t] = t < cl ? jw[0] * fw[0] + jw[1] * fw[1] + jw[2] * fw[2] + jw[3] * fw[3] + jw[4] * fw[4] +
+                                 jw[5] * fw[5]
+                           : 0.0;
+          }
+          for (int r = 0; r < nv; ++r) {
+            const double* h = H1 + 6 * r;
+            double acc = h[0] * fw[0] + h[1] * fw[1] + h[2] * fw[2] + h[3] * fw[3] + h[4] * fw[4] + h[5] * fw[5];
+            const double* pr = Ps + r * nv;
+#pragma unroll
+            for (int t = 0; t < MAXCH; ++t)
+              if (t < cl) acc += pr[dof[t]] * cv[t];
+            out[(int64_t)r * ldp + col] = acc;
+          }
         }
       } else if (col < kp.wy + 2 * nja) {
         const bool coul = col >= kp.wy + nja;
