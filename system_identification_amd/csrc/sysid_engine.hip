@@ -41,7 +41,8 @@ struct sysid_engine {
   // K1
   K1Params kp{};
   uint32_t* d_mimg = nullptr;
-  int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4;
+  unsigned long long* d_work = nullptr;  // K1 sample counter + departed-wave counter (self-resetting)
+  int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4, k1_variant = 0;
   size_t k1_lds = 0;
   // K2/K3 Gram tiling
   int ntc = 0, nslots = 0, nsuper = 0, ngroups = 0;
@@ -104,9 +105,22 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
   return SYSID_OK;
 }
 
-const void* k1_fn(int maxch_tpl) {
-  return maxch_tpl <= 4 ? reinterpret_cast<const void*>(k1_regressor_panel<4>)
-                        : reinterpret_cast<const void*>(k1_regressor_panel<16>);
+// K1 instantiations: chain slots x compile-time nv (quadrupeds: nv = 18; anything else reads nv at
+// run time — a compile-time nv = 35 for the humanoid ran 1.8x slower, its unrolled serial phases
+// being heavier than the saved address arithmetic).
+enum { K1_C4_NV18, K1_C4, K1_C16 };
+
+int k1_variant(int maxch_tpl, int nv) {
+  if (maxch_tpl <= 4) return nv == 18 ? K1_C4_NV18 : K1_C4;
+  return K1_C16;
+}
+
+const void* k1_fn(int variant) {
+  switch (variant) {
+    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<4, 18>);
+    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0>);
+    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0>);
+  }
 }
 
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
@@ -116,12 +130,20 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
   const int64_t waves_needed = N;
   const int64_t cap = (int64_t)e->cus * e->k1_blocks_per_cu;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + e->k1_waves - 1) / e->k1_waves));
-  if (e->k1_maxch_tpl <= 4)
-    hipLaunchKernelGGL(k1_regressor_panel<4>, dim3((unsigned)grid), dim3(64 * e->k1_waves), e->k1_lds, st, kp,
-                       e->d_mimg, d_in, N, ld, d_panel, ld_panel, dbg);
-  else
-    hipLaunchKernelGGL(k1_regressor_panel<16>, dim3((unsigned)grid), dim3(64 * e->k1_waves), e->k1_lds, st, kp,
-                       e->d_mimg, d_in, N, ld, d_panel, ld_panel, dbg);
+  const dim3 g1((unsigned)grid), b1(64 * e->k1_waves);
+  switch (e->k1_variant) {
+    case K1_C4_NV18:
+      hipLaunchKernelGGL((k1_regressor_panel<4, 18>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+                         ld_panel, e->d_work, dbg);
+      break;
+    case K1_C4:
+      hipLaunchKernelGGL((k1_regressor_panel<4, 0>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+                         ld_panel, e->d_work, dbg);
+      break;
+    default:
+      hipLaunchKernelGGL((k1_regressor_panel<16, 0>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+                         ld_panel, e->d_work, dbg);
+  }
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
@@ -304,6 +326,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.thr_rel = 1e-13;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;
+  e->k1_variant = k1_variant(maxch_tpl, nv);
 
   // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
   // K2_WAVES x K2_SPW super slots per workgroup group; 4 tile slots per super slot.
@@ -336,6 +359,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMalloc(&e->d_work, 2 * sizeof(unsigned long long));
+  if (st == hipSuccess) st = hipMemset(e->d_work, 0, 2 * sizeof(unsigned long long));
   if (st == hipSuccess) st = hipMalloc(&e->d_tiles, both.size() * sizeof(int2));
   if (st == hipSuccess) st = hipMemcpy(e->d_tiles, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice);
   // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget
@@ -344,9 +369,9 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     for (int wv : {4, 2, 1}) {
       const size_t lds = (size_t)(MI.ndbl + wv * WL.total) * sizeof(double);
       if (lds > 160 * 1024) continue;
-      (void)hipFuncSetAttribute(k1_fn(maxch_tpl), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute(k1_fn(e->k1_variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k1_fn(maxch_tpl), 64 * wv, lds) != hipSuccess) nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k1_fn(e->k1_variant), 64 * wv, lds) != hipSuccess) nb = 0;
       if (nb * wv > best) { best = nb * wv; e->k1_waves = wv; e->k1_blocks_per_cu = std::max(1, nb); e->k1_lds = lds; }
     }
     if (best <= 0) {
@@ -354,7 +379,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       sysid_destroy(e);
       return SYSID_E_MODEL;
     }
-    st = hipFuncSetAttribute(k1_fn(maxch_tpl), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
+    st = hipFuncSetAttribute(k1_fn(e->k1_variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
   }
   if (st != hipSuccess) {
     set_err(nullptr, SYSID_E_DEVICE, "device setup failed: %s", hipGetErrorString(st));
@@ -369,8 +394,8 @@ void sysid_destroy(sysid_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_tiles, (void*)e->d_in, (void*)e->d_panel, (void*)e->d_gram, e->d_ws,
-                  (void*)e->d_dump})
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->d_tiles, (void*)e->d_in, (void*)e->d_panel,
+                  (void*)e->d_gram, e->d_ws, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;

@@ -225,13 +225,16 @@ __device__ __forceinline__ void wsync() {
 // ------------------------------------------------------------------------------------------------
 // K1
 // ------------------------------------------------------------------------------------------------
-template <int MAXCH>
+// MAXCH: chain-slot count (>= longest revolute chain).  NVC: nv fixed at compile time (0 = read it
+// from K1Params), so the row loops of the common robots unroll with immediate LDS offsets.
+template <int MAXCH, int NVC>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
 #endif
 __global__ void __launch_bounds__(64 * K1_WAVES, SYSID_K1_MIN_WAVES_PER_EU)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
-                   int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp, double* __restrict__ dbg) {
+                   int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp,
+                   unsigned long long* __restrict__ work, double* __restrict__ dbg) {
   extern __shared__ double smem[];
   const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
   {
@@ -257,16 +260,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const double* t0 = smem + MI.t0;
   const double* ct = smem + MI.ct;
 
-  const int nv = kp.nv, nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
+  const int nv = NVC > 0 ? NVC : kp.nv;
+  const int nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const WLay L = wave_layout(IN, nv, NJ, nc);
   double* wr = smem + kp.mimg_dbl + wave * kp.wave_dbl;
-  double* sin_ = wr + L.in;
-  const double* q = sin_;
-  const double* dq = sin_ + nq;
-  const double* ddq = dq + nv;
-  const double* tau = ddq + nv;
-  const double* cnt = tau + nja;
   double* body = wr + L.body;
   double* Ws = wr + L.W;
   double* Pts = wr + L.Pt;
@@ -278,36 +276,51 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   double* H1 = wr + L.H1;
   double* tps = wr + L.tp;
 
-  const int wpb = blockDim.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * wpb + wave;
-  const int64_t TW = (int64_t)gridDim.x * wpb;
-  const int64_t s_begin = gw * N / TW, s_end = (gw + 1) * N / TW;
-  if (s_begin >= s_end) return;  // no workgroup barrier follows
-
-  // inputs of the next sample are prefetched into registers (channel c -> lane c, c+64, c+128)
+  // Samples are handed out one at a time from a device counter (work[0]), so a workgroup that becomes
+  // resident late, or a slow CU, only ever costs its own last sample.  The next index is claimed one
+  // sample ahead, its inputs are prefetched into registers (channel c -> lane c, c+64, c+128) while the
+  // current sample runs.  The last wave to leave resets the counters for the next launch (work[1]
+  // counts departed waves; no wave touches work[0] after its last claim returned >= N).
+  auto claim = [&]() -> int64_t {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(work, 1ull);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (int64_t)(((unsigned long long)hi << 32) | lo);
+  };
   double x0 = 0.0, x1 = 0.0, x2 = 0.0;
   auto fetch = [&](int64_t s) {
     if (lane < IN) x0 = in[(int64_t)lane * ld + s];
     if (lane + 64 < IN) x1 = in[(int64_t)(lane + 64) * ld + s];
     if (lane + 128 < IN) x2 = in[(int64_t)(lane + 128) * ld + s];
   };
-  fetch(s_begin);
+  double* sin_ = wr + L.in;
+  const double* q = sin_;
+  const double* dq = sin_ + nq;
+  const double* ddq = dq + nv;
+  const double* tau = ddq + nv;
+  const double* cnt = tau + nja;
+
+  int64_t s = claim();
+  int64_t s1 = s < N ? claim() : N;
+  if (s < N) fetch(s);
 #ifdef SYSID_STAMPS
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
-  for (int64_t s = s_begin; s < s_end; ++s) {
+  while (s < N) {
     wsync();
     if (lane < IN) sin_[lane] = x0;
     if (lane + 64 < IN) sin_[lane + 64] = x1;
     if (lane + 128 < IN) sin_[lane + 128] = x2;
+    const int64_t s2 = s1 < N ? claim() : N;  // used one sample from now
+    if (s1 < N) fetch(s1);
     if (lane < 24) {
       double v = 0.0;
       if (lane == 0 || lane == 4 || lane == 8) v = 1.0;   // oR_0 = I
       if (lane >= 18 && lane < 21) v = -(lane == 18 ? kp.g0 : (lane == 19 ? kp.g1 : kp.g2));
       body[lane] = v;
     }
-    if (s + 1 < s_end) fetch(s + 1);
     wsync();
     K1_STAMP(0)
 
@@ -548,7 +561,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
             cv[t] = t < cl ? c : 0.0;
             pofs[t] = d;
           }
-#pragma unroll 2
+          constexpr int RU = NVC > 0 ? 3 : 2;
+#pragma unroll RU
           for (int r = 0; r < nv; ++r) {
             const double* h = H1 + 6 * r;
             const double* pr = Ps + r * nv;
@@ -595,6 +609,15 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
     }
     K1_STAMP(7)
+    s = s1;
+    s1 = s2;
+  }
+  if (lane == 0) {
+    const unsigned long long total = (unsigned long long)gridDim.x * (blockDim.x >> 6);
+    if (atomicAdd(work + 1, 1ull) == total - 1) {
+      work[0] = 0;
+      work[1] = 0;
+    }
   }
 }
 

@@ -5,7 +5,7 @@ reads; both the raw value and the x2-corrected value are reported."""
 import collections, csv, json, re, sys
 
 def kname(s):
-    m = re.search(r"::(\w+)\(", s)
+    m = re.search(r"::(\w+?)(<[^(]*>)?\(", s)
     return m.group(1) if m else s.split("(")[0]
 
 d = sys.argv[1]

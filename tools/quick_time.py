@@ -20,3 +20,8 @@ bytes_k1 = N * ((m.nq + 2 * m.nv + m.nj + m.n_ee) * 8 + m.nv * (eng.w + 1) * 8)
 W = eng.w
 flops_k2 = N * (m.nv * W * (W + 1) + 2 * m.nv * W)
 print("K1 %.1f GB/s   K2 %.2f TF/s   samples/s %.3e" % (bytes_k1 / ms[0] / 1e6, flops_k2 / ms[1] / 1e9, N / sum(ms) * 1e3))
+import ctypes
+from system_identification_amd import engine as _E
+cfg = (ctypes.c_int32 * 4)()
+eng.lib.sysid_debug_k1_config(eng._h, cfg)
+print("k1 config [waves/block, blocks/CU, lds bytes, maxch]:", list(cfg))
