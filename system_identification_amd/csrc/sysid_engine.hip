@@ -323,6 +323,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
   kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL.total; kp.out_cols = e->ldp;
+  kp.rg = std::max(1, 64 / std::max(1, NJ - 1));
   kp.thr_rel = 1e-13;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;
@@ -452,6 +453,8 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
     return set_err(e, SYSID_E_INVALID, "bad arguments (N=%lld ld=%lld ld_panel=%lld, need an even ld_panel >= %d)",
                    (long long)N, (long long)ld, (long long)ld_panel, e->ncol);
   if ((flags & SYSID_EMIT_GRAM) && !d_gram) return set_err(e, SYSID_E_INVALID, "EMIT_GRAM without gram buffer");
+  if (reinterpret_cast<uintptr_t>(d_panel) & 15)
+    return set_err(e, SYSID_E_INVALID, "d_panel must be 16-byte aligned (the panel is written with 16-byte stores)");
   HIP_TRY(e, hipSetDevice(e->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (N == 0) {
@@ -559,7 +562,9 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
 
 int32_t sysid_debug_body_column(const double* body24, int32_t p, double* fw6) {
   if (!body24 || !fw6 || p < 0 || p > 9) return SYSID_E_INVALID;
-  body_regressor_world_column(body24, p, fw6);
+  double F[FBLK];
+  body_regressor_block(body24, F);
+  block_column(F, p, fw6);
   return SYSID_OK;
 }
 

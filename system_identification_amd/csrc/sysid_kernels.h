@@ -85,6 +85,7 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc)
 struct K1Params {
   int nq, nv, NJ, nc, bd, nj, maxdepth, wy, w, ncol, in_rows, maxch, has_ff, ff0, mimg_dbl, wave_dbl;
   int out_cols;     // columns written per panel row (ncol rounded up to the panel's even stride)
+  int rg;           // row groups of the regressor-column phase (lanes = bodies x rg)
   double thr_rel;   // Cholesky pivot cut (relative to max diag(J_c J_c^T))
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
 };
@@ -161,47 +162,6 @@ __device__ inline double sign_of(double x) {
   return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == x ? 0.0 : x));
 }
 
-// Column p of pinocchio's bodyRegressor(v, a_gf) (parameters [m, mc, Ixx, Ixy, Iyy, Ixz, Iyz, Izz];
-// force rows [f; n]) moved to the world frame: fw = oX_i^* f.  bi = {oR(9), ot(3), v(6), a_gf(6)}.
-// Branch-free: every lane of a wave runs the same instructions whatever its column p.
-__host__ __device__ inline void body_regressor_world_column(const double* bi, int p, double* fw) {
-  const double* v = bi + 12;
-  const double* a = bi + 18;
-  const double* w = v + 3;
-  const double* dw = a + 3;
-  double ac[3], tmp[3];
-  cross3(w, v, tmp);
-  ac[0] = a[0] + tmp[0]; ac[1] = a[1] + tmp[1]; ac[2] = a[2] + tmp[2];
-  const double sm = p == 0 ? 1.0 : 0.0;
-  const double e[3] = {p == 1 ? 1.0 : 0.0, p == 2 ? 1.0 : 0.0, p == 3 ? 1.0 : 0.0};
-  const double s0 = p == 4 ? 1.0 : 0.0, s1 = p == 5 ? 1.0 : 0.0, s2 = p == 6 ? 1.0 : 0.0;
-  const double s3 = p == 7 ? 1.0 : 0.0, s4 = p == 8 ? 1.0 : 0.0, s5 = p == 9 ? 1.0 : 0.0;
-  // f = m ac + (dw x + w x w x) h ;  n = h x ac + I dw + w x (I w)
-  double x1[3], x2[3], x3[3], n[3], f[3];
-  cross3(dw, e, x1);
-  cross3(w, e, x2);
-  cross3(w, x2, x3);
-  f[0] = sm * ac[0] + x1[0] + x3[0];
-  f[1] = sm * ac[1] + x1[1] + x3[1];
-  f[2] = sm * ac[2] + x1[2] + x3[2];
-  cross3(e, ac, n);
-  double bdw[3], bw[3];
-  bdw[0] = s0 * dw[0] + s1 * dw[1] + s3 * dw[2];
-  bdw[1] = s1 * dw[0] + s2 * dw[1] + s4 * dw[2];
-  bdw[2] = s3 * dw[0] + s4 * dw[1] + s5 * dw[2];
-  bw[0] = s0 * w[0] + s1 * w[1] + s3 * w[2];
-  bw[1] = s1 * w[0] + s2 * w[1] + s4 * w[2];
-  bw[2] = s3 * w[0] + s4 * w[1] + s5 * w[2];
-  cross3(w, bw, x2);
-  n[0] += bdw[0] + x2[0];
-  n[1] += bdw[1] + x2[1];
-  n[2] += bdw[2] + x2[2];
-  double nl[3];
-  mat3vec(bi, f, fw);
-  mat3vec(bi, n, nl);
-  cross3(bi + 9, fw, tmp);
-  fw[3] = nl[0] + tmp[0]; fw[4] = nl[1] + tmp[1]; fw[5] = nl[2] + tmp[2];
-}
 
 // Wave-level ordering point for LDS traffic.  The LDS executes one wave's DS instructions in issue
 // order, so a store by one lane is seen by a later load of any lane of the same wave; this only stops
@@ -212,15 +172,83 @@ __device__ __forceinline__ void wsync() {
 }
 
 #ifdef SYSID_STAMPS
+// Diagnostics build: per-phase shader-clock deltas accumulated in registers (s_memtime is uniform, so
+// every lane holds the same values) and added to dbg[0..7] once per wave at exit.
 #define K1_STAMP(k)                                                                                 \
-  if (lane == 0) {                                                                                  \
+  {                                                                                                 \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                                     \
-    atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + (k), _t - t_prev);                      \
+    t_acc[k] += _t - t_prev;                                                                        \
     t_prev = _t;                                                                                    \
   }
 #else
 #define K1_STAMP(k)
 #endif
+
+// All ten columns of pinocchio's bodyRegressor for body i, moved to the free-flyer frame, in a compact
+// layout: columns 0..3 (m, mc) as [linear(3); angular(3)] in F[0..23]; columns 4..9 (inertia) have a
+// zero force part, only their angular rows are kept in F[24..41].  bi = {oR(9), ot(3), v(6), a_gf(6)}.
+constexpr int FBLK = 42;
+
+__host__ __device__ inline void body_regressor_block(const double* bi, double* F) {
+  const double* R = bi;
+  const double* t = bi + 9;
+  const double* v = bi + 12;
+  const double* w = bi + 15;
+  const double* a = bi + 18;
+  const double* dw = bi + 21;
+  double ac[3], tmp[3];
+  cross3(w, v, tmp);
+  ac[0] = a[0] + tmp[0]; ac[1] = a[1] + tmp[1]; ac[2] = a[2] + tmp[2];
+  // column 0 (mass): f = ac, n = 0
+  {
+    double Rf[3];
+    mat3vec(R, ac, Rf);
+    F[0] = Rf[0]; F[1] = Rf[1]; F[2] = Rf[2];
+    cross3(t, Rf, F + 3);
+  }
+  // columns 1..3 (first moment e_k): f = dw x e + w x (w x e), n = e x ac
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double e[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
+    double x1[3], x2[3], x3[3], f[3], n[3], Rf[3], Rn[3], tf[3];
+    cross3(dw, e, x1);
+    cross3(w, e, x2);
+    cross3(w, x2, x3);
+    f[0] = x1[0] + x3[0]; f[1] = x1[1] + x3[1]; f[2] = x1[2] + x3[2];
+    cross3(e, ac, n);
+    mat3vec(R, f, Rf);
+    mat3vec(R, n, Rn);
+    cross3(t, Rf, tf);
+    double* c = F + 6 * (k + 1);
+    c[0] = Rf[0]; c[1] = Rf[1]; c[2] = Rf[2];
+    c[3] = Rn[0] + tf[0]; c[4] = Rn[1] + tf[1]; c[5] = Rn[2] + tf[2];
+  }
+  // columns 4..9 (Ixx, Ixy, Iyy, Ixz, Iyz, Izz): f = 0, n = I dw + w x (I w)
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const double s0 = q == 0, s1 = q == 1, s2 = q == 2, s3 = q == 3, s4 = q == 4, s5 = q == 5;
+    double bdw[3], bw[3], x[3], n[3];
+    bdw[0] = s0 * dw[0] + s1 * dw[1] + s3 * dw[2];
+    bdw[1] = s1 * dw[0] + s2 * dw[1] + s4 * dw[2];
+    bdw[2] = s3 * dw[0] + s4 * dw[1] + s5 * dw[2];
+    bw[0] = s0 * w[0] + s1 * w[1] + s3 * w[2];
+    bw[1] = s1 * w[0] + s2 * w[1] + s4 * w[2];
+    bw[2] = s3 * w[0] + s4 * w[1] + s5 * w[2];
+    cross3(w, bw, x);
+    n[0] = bdw[0] + x[0]; n[1] = bdw[1] + x[1]; n[2] = bdw[2] + x[2];
+    mat3vec(R, n, F + 24 + 3 * q);
+  }
+}
+
+// Column p of the block as a 6-vector [linear; angular] (diagnostics and tests).
+__host__ __device__ inline void block_column(const double* F, int p, double* fw) {
+  if (p < 4) {
+    for (int k = 0; k < 6; ++k) fw[k] = F[6 * p + k];
+  } else {
+    fw[0] = fw[1] = fw[2] = 0.0;
+    for (int k = 0; k < 3; ++k) fw[3 + k] = F[24 + 3 * (p - 4) + k];
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // K1
@@ -305,6 +333,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   int64_t s1 = s < N ? claim() : N;
   if (s < N) fetch(s);
 #ifdef SYSID_STAMPS
+  unsigned long long t_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -324,34 +353,49 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     K1_STAMP(0)
 
-    // ---- forward pass (computeJointTorqueRegressor forward step) + world placements ----
+    // ---- forward pass (computeJointTorqueRegressor forward step) + placements ----
+    // Joint placements liMi = jointPlacement * M_J(q) of every joint at once (one lane per joint: the
+    // sincos / quaternion work is off the depth-serial path), parked in the joint's own pose slot.
+    for (int j = 1 + lane; j < NJ; j += 64) {
+      const int iq = idx_q[j];
+      double RJ[9], tJ[3];
+      if (jtype[j] == JT_FREEFLYER) {
+        quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], RJ);
+        tJ[0] = q[iq]; tJ[1] = q[iq + 1]; tJ[2] = q[iq + 2];
+      } else {
+        axis_rotation(axis + 3 * j, q[iq], RJ);
+        tJ[0] = tJ[1] = tJ[2] = 0.0;
+      }
+      double* bj = body + 24 * j;
+      double tmp[3];
+      mat3mul(R0 + 9 * j, RJ, bj);
+      mat3vec(R0 + 9 * j, tJ, tmp);
+      bj[9] = tmp[0] + t0[3 * j]; bj[10] = tmp[1] + t0[3 * j + 1]; bj[11] = tmp[2] + t0[3 * j + 2];
+    }
+    wsync();
+    // Velocities / accelerations level by level (a joint's parent is one level up).
     for (int lvl = 1; lvl <= kp.maxdepth; ++lvl) {
       for (int j = 1 + lane; j < NJ; j += 64) {
         if (depth[j] != lvl) continue;
         const int p = parent[j];
-        const int iq = idx_q[j], iv = idx_v[j];
+        const int iv = idx_v[j];
         const double* bp = body + 24 * p;
         double* bj = body + 24 * j;
-        double RJ[9], tJ[3], vJ[6], Sa[6];
+        double liR[9], lit[3], vJ[6], Sa[6];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) liR[k] = bj[k];
+        lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
         const bool ff = jtype[j] == JT_FREEFLYER;
         if (ff) {
-          quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], RJ);
-          tJ[0] = q[iq]; tJ[1] = q[iq + 1]; tJ[2] = q[iq + 2];
 #pragma unroll
           for (int k = 0; k < 6; ++k) { vJ[k] = dq[iv + k]; Sa[k] = ddq[iv + k]; }
         } else {
           const double* ax = axis + 3 * j;
-          axis_rotation(ax, q[iq], RJ);
-          tJ[0] = tJ[1] = tJ[2] = 0.0;
           const double w = dq[iv], aa = ddq[iv];
           vJ[0] = vJ[1] = vJ[2] = 0.0; Sa[0] = Sa[1] = Sa[2] = 0.0;
           vJ[3] = ax[0] * w; vJ[4] = ax[1] * w; vJ[5] = ax[2] * w;
           Sa[3] = ax[0] * aa; Sa[4] = ax[1] * aa; Sa[5] = ax[2] * aa;
         }
-        double liR[9], lit[3], tmp[3];
-        mat3mul(R0 + 9 * j, RJ, liR);
-        mat3vec(R0 + 9 * j, tJ, tmp);
-        lit[0] = tmp[0] + t0[3 * j]; lit[1] = tmp[1] + t0[3 * j + 1]; lit[2] = tmp[2] + t0[3 * j + 2];
         double vp[6], ap[6], vi[6], ai[6], c1[3], c2[3];
         act_inv_motion(liR, lit, bp + 12, vp);
         act_inv_motion(liR, lit, bp + 18, ap);
@@ -538,80 +582,92 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     K1_STAMP(6)
 
-    // ---- panel columns: [Y_proj | B_v | B_c | tau_proj | pad] ----
+    // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
+    // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
+    // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
+    // One G row (6 + 6*chain FMAs) feeds 42 FMAs and five 16-byte stores.
     double* out = panel + (s * nv) * ldp;
-    for (int col = lane; col < kp.out_cols; col += 64) {
-      if (col < kp.wy) {
-        const int i = col / 10 + 1, p = col - 10 * (col / 10);
-        double fw[6];
-        body_regressor_world_column(body + 24 * i, p, fw);
-        // revolute ancestors of body i (and i): c_t = J_w[:, dof_t] . fw
-        const int cl = chain_len[i];
-        if constexpr (MAXCH <= 8) {
-          // short chains: unused slots read a valid P column with a zero coefficient, so the row
-          // loop has no branch and all of its LDS reads are in flight together
-          int pofs[MAXCH];
-          double cv[MAXCH];
+    const int nbody = NJ - 1, nyi = nbody * kp.rg;
+    for (int it = lane; it < nyi; it += 64) {
+      const int g = it / nbody, i = it - g * nbody + 1;
+      const int r0 = g * nv / kp.rg, r1 = (g + 1) * nv / kp.rg;
+      double F[FBLK];
+      body_regressor_block(body + 24 * i, F);
+      const int cl = chain_len[i];
+      int dof[MAXCH <= 4 ? MAXCH : 1];  // short chains: dofs read once, a row's loads issue together
+      if constexpr (MAXCH <= 4) {
+#pragma unroll
+        for (int t = 0; t < MAXCH; ++t) dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
+      }
+      double* oi = out + 10 * (i - 1);
+      for (int r = r0; r < r1; ++r) {
+        const double* h = H1 + 6 * r;
+        const double* pr = Ps + r * nv;
+        double G[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) G[k] = h[k];
+        if constexpr (MAXCH <= 4) {
 #pragma unroll
           for (int t = 0; t < MAXCH; ++t) {
-            const int d = t < cl ? chain[i * kp.maxch + t] : 0;
-            const double* jw = Jws + 6 * d;
-            const double c = jw[0] * fw[0] + jw[1] * fw[1] + jw[2] * fw[2] + jw[3] * fw[3] + jw[4] * fw[4] +
-                             jw[5] * fw[5];
-            cv[t] = t < cl ? c : 0.0;
-            pofs[t] = d;
-          }
-          constexpr int RU = NVC > 0 ? 3 : 2;
-#pragma unroll RU
-          for (int r = 0; r < nv; ++r) {
-            const double* h = H1 + 6 * r;
-            const double* pr = Ps + r * nv;
-            double pv[MAXCH];
+            if (t < cl) {
+              const double pv = pr[dof[t]];
+              const double* jw = Jws + 6 * dof[t];
 #pragma unroll
-            for (int t = 0; t < MAXCH; ++t) pv[t] = pr[pofs[t]];
-            double acc = h[0] * fw[0] + h[1] * fw[1] + h[2] * fw[2] + h[3] * fw[3] + h[4] * fw[4] + h[5] * fw[5];
-#pragma unroll
-            for (int t = 0; t < MAXCH; ++t) acc += pv[t] * cv[t];
-            out[(int64_t)r * ldp + col] = acc;
+              for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
+            }
           }
         } else {
-          // long chains (humanoids): predicated terms keep the register footprint bounded
-          int dof[MAXCH];
-          double cv[MAXCH];
+          for (int t = 0; t < cl; ++t) {
+            const int d = chain[i * kp.maxch + t];
+            const double pv = pr[d];
+            const double* jw = Jws + 6 * d;
 #pragma unroll
-          for (int t = 0; t < MAXCH; ++t) {
-            dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
-            const double* jw = Jws + 6 * dof[t];
-            cv[t] = t < cl ? jw[0] * fw[0] + jw[1] * fw[1] + jw[2] * fw[2] + jw[3] * fw[3] + jw[4] * fw[4] +
-                                 jw[5] * fw[5]
-                           : 0.0;
-          }
-          for (int r = 0; r < nv; ++r) {
-            const double* h = H1 + 6 * r;
-            double acc = h[0] * fw[0] + h[1] * fw[1] + h[2] * fw[2] + h[3] * fw[3] + h[4] * fw[4] + h[5] * fw[5];
-            const double* pr = Ps + r * nv;
-#pragma unroll
-            for (int t = 0; t < MAXCH; ++t)
-              if (t < cl) acc += pr[dof[t]] * cv[t];
-            out[(int64_t)r * ldp + col] = acc;
+            for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
           }
         }
-      } else if (col < kp.wy + 2 * nja) {
-        const bool coul = col >= kp.wy + nja;
-        const int jj = col - kp.wy - (coul ? nja : 0);
-        const double x = dq[bd + jj];
-        const double sc = coul ? sign_of(x) : x;
-        for (int r = 0; r < nv; ++r) out[(int64_t)r * ldp + col] = Ps[r * nv + bd + jj] * sc;
-      } else if (col == kp.w) {
-        for (int r = 0; r < nv; ++r) out[(int64_t)r * ldp + col] = tps[r];
-      } else {
-        for (int r = 0; r < nv; ++r) out[(int64_t)r * ldp + col] = 0.0;  // pad: keep lines whole
+        double y[10];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          y[c] = G[0] * F[6 * c] + G[1] * F[6 * c + 1] + G[2] * F[6 * c + 2] + G[3] * F[6 * c + 3] +
+                 G[4] * F[6 * c + 4] + G[5] * F[6 * c + 5];
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+          y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
+        double2* o2 = reinterpret_cast<double2*>(oi + (int64_t)r * ldp);
+#pragma unroll
+        for (int c = 0; c < 5; ++c) o2[c] = make_double2(y[2 * c], y[2 * c + 1]);
+      }
+    }
+
+    // ---- [B_v | B_c | tau_proj | pad]: lane = (row, column pair), 16-byte stores ----
+    {
+      const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
+      for (int it = lane; it < nv * npair; it += 64) {
+        const int r = it / npair, m = it - r * npair;
+        const double* pr = Ps + r * nv + bd;
+        double v2[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int jj = 2 * m + u;                      // column - wy
+          const bool coul = jj >= nja;
+          const int j = coul ? jj - nja : jj;
+          const int jc = j < nja ? j : nja - 1;          // clamp for the tau/pad columns
+          const double x = dq[bd + jc];
+          const double sc = coul ? sign_of(x) : x;
+          const double fr = pr[jc] * sc;
+          v2[u] = jj < 2 * nja ? fr : (kp.wy + jj == kp.w ? tps[r] : 0.0);  // pad: keep lines whole
+        }
+        *reinterpret_cast<double2*>(out + (int64_t)r * ldp + kp.wy + 2 * m) = make_double2(v2[0], v2[1]);
       }
     }
     K1_STAMP(7)
     s = s1;
     s1 = s2;
   }
+#ifdef SYSID_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + k, t_acc[k]);
+#endif
   if (lane == 0) {
     const unsigned long long total = (unsigned long long)gridDim.x * (blockDim.x >> 6);
     if (atomicAdd(work + 1, 1ull) == total - 1) {
@@ -790,7 +846,9 @@ __global__ void debug_body_column_kernel(const double* __restrict__ body24, doub
   if (threadIdx.x < 24) b[threadIdx.x] = body24[threadIdx.x];
   __syncthreads();
   double fw[6];
-  body_regressor_world_column(b, threadIdx.x % 10, fw);
+  double F[FBLK];
+  body_regressor_block(b, F);
+  block_column(F, threadIdx.x % 10, fw);
   for (int k = 0; k < 6; ++k) out[threadIdx.x * 6 + k] = fw[k];
 }
 
