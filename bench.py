@@ -37,6 +37,25 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel, robot, samples):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary for this workload
+    (profiles/<round>/pmc_summary.json: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        cfg = d.get("_config", {})
+        if cfg.get("robot") != robot or cfg.get("samples") != samples or kernel not in d:
+            continue
+        k = d[kernel]
+        if "FETCH_bytes_corrected_x2" in k and "WRITE_bytes" in k:
+            return round(k["FETCH_bytes_corrected_x2"] + k["WRITE_bytes"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(model, data, n_sample):
     """The C restatement of the reference path (oracle/sysid_oracle.c), one thread, on n_sample samples."""
     from oracle.ref_c import COracle
@@ -108,14 +127,16 @@ def main():
     k1_gbs = N * bytes_k1 / (ms[0] * 1e-3) / 1e9
     k2_tfs = N * flops_k2 / (ms[1] * 1e-3) / 1e12
     if ms[0] >= ms[1]:
-        roof = {"kernel": "regressor_panel_kernel (K1)", "bound": "hbm", "achieved": round(k1_gbs, 1),
+        traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N)
+        roof = {"kernel": "k1_regressor_panel", "bound": "hbm", "achieved": round(k1_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
-                "traffic": None, "algorithmic_bytes_per_launch": N * bytes_k1,
+                "traffic": traffic, "traffic_source": src, "algorithmic_bytes_per_launch": N * bytes_k1,
                 "avg_launch_ms": round(ms[0], 5)}
     else:
-        roof = {"kernel": "gram_syrk_kernel (K2)", "bound": "mfma", "achieved": round(k2_tfs, 3),
+        traffic, src = pmc_traffic("k2_gram_syrk", args.robot, N)
+        roof = {"kernel": "k2_gram_syrk", "bound": "mfma", "achieved": round(k2_tfs, 3),
                 "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(k2_tfs / FP64_MFMA_PEAK_TFS, 4),
-                "traffic": None, "algorithmic_flops_per_launch": N * flops_k2,
+                "traffic": traffic, "traffic_source": src, "algorithmic_flops_per_launch": N * flops_k2,
                 "avg_launch_ms": round(ms[1], 5)}
 
     total_samples = N * world * args.steps
