@@ -31,7 +31,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--robot", default="spot")
     ap.add_argument("--samples", type=int, default=20000, help="samples per GPU")
-    ap.add_argument("--gram-only", action="store_true", help="skip nothing: panel still written (v1)")
+    ap.add_argument("--gram-only", action="store_true",
+                    help="normal equations only (SURVEY.md §8d config 5): the panel is produced chunk by chunk on "
+                         "the device and never returned")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="extra all-core C oracle timing (0 = off)")
     return ap.parse_args()
@@ -93,13 +95,21 @@ def main():
     eng = Engine(model, device=local)
     d_in = torch.from_numpy(channel_block(data)).cuda(local)
     flags = EMIT_ALL
-    bufs = eng.alloc_device(N, flags)
     stream = torch.cuda.current_stream(local)
+    if args.gram_only:
+        bufs = eng.alloc_gram_device(N)
 
-    def step():
-        eng.build_device(d_in, N, flags, bufs, stream=stream.cuda_stream)
-        if world > 1:
-            dist.all_reduce(bufs["gram"])
+        def step():
+            eng.build_gram_device(d_in, N, bufs, stream=stream.cuda_stream)
+            if world > 1:
+                dist.all_reduce(bufs["gram"])
+    else:
+        bufs = eng.alloc_device(N, flags)
+
+        def step():
+            eng.build_device(d_in, N, flags, bufs, stream=stream.cuda_stream)
+            if world > 1:
+                dist.all_reduce(bufs["gram"])
 
     for _ in range(args.warmup):
         step()
@@ -119,24 +129,32 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel device time (HIP events on the engine's stream), for the roofline
-    ms = eng.time_stages(d_in, N, flags, bufs, iters=max(5, args.steps))
+    # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only runs the
+    # same kernels chunk by chunk; they are timed on one chunk-sized batch.
+    n_time = N
+    if args.gram_only:
+        n_time = min(N, max(4096, (512 << 20) // (model.nv * eng.panel_ld * 8)))
+        tb = eng.alloc_device(n_time, flags)
+        ms = eng.time_stages(d_in, n_time, flags, tb, iters=max(5, args.steps))
+        del tb
+    else:
+        ms = eng.time_stages(d_in, N, flags, bufs, iters=max(5, args.steps))
     nv, W = model.nv, eng.w
     bytes_k1 = (model.nq + 2 * nv + model.nj + model.n_ee) * 8 + nv * (W + 1) * 8   # SURVEY §8d per sample
     flops_k2 = nv * W * (W + 1) + 2 * nv * W                                       # SYRK + Aᵀb per sample
-    k1_gbs = N * bytes_k1 / (ms[0] * 1e-3) / 1e9
-    k2_tfs = N * flops_k2 / (ms[1] * 1e-3) / 1e12
+    k1_gbs = n_time * bytes_k1 / (ms[0] * 1e-3) / 1e9
+    k2_tfs = n_time * flops_k2 / (ms[1] * 1e-3) / 1e12
     if ms[0] >= ms[1]:
-        traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N)
+        traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N) if not args.gram_only else (None, None)
         roof = {"kernel": "k1_regressor_panel", "bound": "hbm", "achieved": round(k1_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "traffic_source": src, "algorithmic_bytes_per_launch": N * bytes_k1,
+                "traffic": traffic, "traffic_source": src, "algorithmic_bytes_per_launch": n_time * bytes_k1,
                 "avg_launch_ms": round(ms[0], 5)}
     else:
-        traffic, src = pmc_traffic("k2_gram_syrk", args.robot, N)
+        traffic, src = pmc_traffic("k2_gram_syrk", args.robot, N) if not args.gram_only else (None, None)
         roof = {"kernel": "k2_gram_syrk", "bound": "mfma", "achieved": round(k2_tfs, 3),
                 "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(k2_tfs / FP64_MFMA_PEAK_TFS, 4),
-                "traffic": traffic, "traffic_source": src, "algorithmic_flops_per_launch": N * flops_k2,
+                "traffic": traffic, "traffic_source": src, "algorithmic_flops_per_launch": n_time * flops_k2,
                 "avg_launch_ms": round(ms[1], 5)}
 
     total_samples = N * world * args.steps
@@ -147,12 +165,14 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (SURVEY.md §8d recipe: sinusoidal joints in URDF limits, wobbling base, "
                 "inverse-dynamics torques + noise, trot contacts with LOST=2); no .dat ships with the reference",
-        "config": {"workload": f"{args.robot} {N} samples per GPU, full outputs (stacked Y_proj/tau_proj/"
-                               "B_v/B_c panel + Gram)", "robot": args.robot, "samples_per_gpu": N,
+        "config": {"workload": f"{args.robot} {N} samples per GPU, " + (
+                       "Gram only (panel chunked on the device)" if args.gram_only else
+                       "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
+                   "robot": args.robot, "samples_per_gpu": N,
                    "nv": nv, "W": W, "parallelism": f"dp{world}"},
         "gram_gflops": round(N * world * flops_k2 / (elapsed / args.steps) / 1e9, 2),
         "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
-                      "K3_gram_reduce": round(ms[2], 5)},
+                      "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},
         "K1_GBps": round(k1_gbs, 1), "K2_TFps": round(k2_tfs, 3),
         "roofline": roof,
     }

@@ -23,7 +23,9 @@
  *     numpy broadcast error there) with SYSID_E_CONTACT.
  *   - Return codes: 0 = OK, < 0 = error; nothing is thrown across the ABI.  sysid_last_error() gives
  *     a message.  Python maps E_INVALID/E_MODEL/E_CONTACT to ValueError, E_DEVICE/E_NOMEM to RuntimeError.
- *   - A handle is bound to one device and owns one HIP stream; it is not re-entrant across threads.
+ *   - A handle is bound to one device and owns one HIP stream; it is not re-entrant across threads,
+ *     and at most one of its device launches may be in flight at a time (its K1 sample counter is
+ *     per handle): stream-order the calls of one handle, use one handle per concurrent stream.
  *
  * Packed model (produced by system_identification_amd.model.Model.pack()), little endian:
  *   int32  header[16] = {0x44495953 'SYID', version 1, nq, nv, njoints, n_contact, base_dof, nj, 0...}
@@ -66,7 +68,7 @@ extern "C" {
 typedef struct sysid_engine sysid_engine;
 
 /* ABI version (bumped on any signature or layout change). */
-int32_t sysid_abi_version(void);
+int32_t sysid_abi_version(void);  /* 3 */
 
 /* Create an engine for one device from a packed model.  Replaces the model construction of
  * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
@@ -85,7 +87,8 @@ int32_t sysid_dims(const sysid_engine* e, int32_t* nq, int32_t* nv, int32_t* nj,
  *   q (nq x ld), dq/ddq (nv x ld), tau (nj x ld), cnt (n_contact x ld): float64, channel-major.
  *   Y_proj (N·nv x 10·nb), tau_proj (N·nv), B_v/B_c (N·nv x nj): row-major, caller-allocated;
  *   gram (W x W), Atb (W), btb (1).  Any output may be NULL ("don't emit"); flags select work.
- * Synchronous: returns after all outputs are in host memory. */
+ * Synchronous: returns after all outputs are in host memory.  With SYSID_EMIT_GRAM and no stacked output
+ * requested the panel is never materialised in full (the Gram-only path of sysid_build_gram_device). */
 int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const double* ddq,
                     const double* tau, const double* cnt, int64_t N, int64_t ld, uint32_t flags,
                     double* Y_proj, double* tau_proj, double* B_v, double* B_c,
@@ -103,6 +106,15 @@ size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags);
 int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
                            double* d_panel, int64_t ld_panel, double* d_gram,
                            void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* Gram-only device entry point ("K1 fused with K2"): normal equations of N samples
+ * without the N·nv-row panel.  The panel is produced in chunks of about 512 MiB inside the workspace
+ * and folded into the same Gram accumulators chunk after chunk; d_gram as in sysid_build_device.
+ * Replaces what Solver.__init__ (src/solver.py:6-29) needs from the stacked arrays: G, g, bᵀb and
+ * num_rows = N·nv (the objective scale of :190).  Stream-ordered, no allocation. */
+size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N);
+int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram,
+                                void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Host-side check of the contact contract for n_contact x ld contact values (SYSID_E_CONTACT on the
  * first offending sample, whose index is written to *bad_sample when non-NULL). */

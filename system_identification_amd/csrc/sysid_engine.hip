@@ -148,6 +148,43 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
   return SYSID_OK;
 }
 
+int launch_k2(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
+              double* slab, hipStream_t st) {
+  if (ld_panel > 16 * e->ntc)
+    return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
+  const dim3 g2(e->ngroups * ks), b2(64 * K2_WAVES);
+  switch (e->ntc) {
+#define SYSID_K2_CASE(NTC, KC)                                                                               \
+  case NTC:                                                                                                 \
+    hipLaunchKernelGGL((k2_gram_syrk<NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles, e->ngroups,  \
+                       ks, e->nslots, accumulate, slab);                                                    \
+    break;
+    SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
+    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
+    SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20)
+    SYSID_K2_CASE(15, 20) SYSID_K2_CASE(16, 16) SYSID_K2_CASE(17, 16) SYSID_K2_CASE(18, 16)
+    SYSID_K2_CASE(19, 16) SYSID_K2_CASE(20, 16) SYSID_K2_CASE(21, 12) SYSID_K2_CASE(22, 12)
+    SYSID_K2_CASE(23, 12) SYSID_K2_CASE(24, 12)
+#undef SYSID_K2_CASE
+    default:
+      return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
+  }
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
+}
+
+int launch_k3(sysid_engine* e, int ks, const double* slab, double* part, double* d_gram, hipStream_t st) {
+  const int rs = rsplit_for(ks);
+  const int64_t nx = (int64_t)e->nslots * 256;
+  hipLaunchKernelGGL(k3_gram_partial, dim3((unsigned)((nx + 255) / 256), rs), dim3(256), 0, st, slab, nx, ks, rs,
+                     part);
+  HIP_TRY(e, hipGetLastError());
+  hipLaunchKernelGGL(k3_gram_final, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, part,
+                     e->d_tiles + e->nsuper, e->nslots, rs, e->ncol, d_gram);
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
+}
+
 int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                   int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, hipStream_t st,
                   hipEvent_t* ev /* 4 events or null */) {
@@ -158,40 +195,15 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   if (rc != SYSID_OK) return rc;
   if (ev) HIP_TRY(e, hipEventRecord(ev[1], st));
   if (flags & SYSID_EMIT_GRAM) {
-    const int ks = ksplit_for(e, rows), rs = rsplit_for(ks);
+    const int ks = ksplit_for(e, rows);
     const size_t sb = slab_bytes(e, rows), pb = part_bytes(e, rows);
     if (d_ws == nullptr || ws_bytes < sb + pb)
       return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, sb + pb);
     double* slab = static_cast<double*>(d_ws);
     double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + sb);
-    if (ld_panel > 16 * e->ntc)
-      return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
-    const dim3 g2(e->ngroups * ks), b2(64 * K2_WAVES);
-    switch (e->ntc) {
-#define SYSID_K2_CASE(NTC, KC)                                                                               \
-  case NTC:                                                                                                 \
-    hipLaunchKernelGGL((k2_gram_syrk<NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles, e->ngroups,  \
-                       ks, e->nslots, slab);                                                                \
-    break;
-      SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
-      SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
-      SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20)
-      SYSID_K2_CASE(15, 20) SYSID_K2_CASE(16, 16) SYSID_K2_CASE(17, 16) SYSID_K2_CASE(18, 16)
-      SYSID_K2_CASE(19, 16) SYSID_K2_CASE(20, 16) SYSID_K2_CASE(21, 12) SYSID_K2_CASE(22, 12)
-      SYSID_K2_CASE(23, 12) SYSID_K2_CASE(24, 12)
-#undef SYSID_K2_CASE
-      default:
-        return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
-    }
-    HIP_TRY(e, hipGetLastError());
+    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
-    const int64_t nx = (int64_t)e->nslots * 256;
-    hipLaunchKernelGGL(k3_gram_partial, dim3((unsigned)((nx + 255) / 256), rs), dim3(256), 0, st, slab, nx, ks, rs,
-                       part);
-    HIP_TRY(e, hipGetLastError());
-    hipLaunchKernelGGL(k3_gram_final, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, part,
-                       e->d_tiles + e->nsuper, e->nslots, rs, e->ncol, d_gram);
-    HIP_TRY(e, hipGetLastError());
+    if ((rc = launch_k3(e, ks, slab, part, d_gram, st)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
   } else if (ev) {
     HIP_TRY(e, hipEventRecord(ev[2], st));
@@ -200,11 +212,44 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   return SYSID_OK;
 }
 
+// Gram-only: the panel never leaves the device and is produced chunk by chunk into the workspace
+// (about 512 MiB per chunk); K2 accumulates every chunk into the same slabs, K3 reduces once.
+int64_t gram_chunk(const sysid_engine* e, int64_t N) {
+  const int64_t per = (int64_t)e->nv * e->ldp * (int64_t)sizeof(double);
+  const int64_t c = std::max<int64_t>(4096, (512ll << 20) / per);
+  return std::max<int64_t>(1, std::min(c, N));
+}
+
+size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {
+  const int64_t rows = gram_chunk(e, N) * e->nv;
+  return align256((size_t)rows * e->ldp * sizeof(double)) + slab_bytes(e, rows) + part_bytes(e, rows);
+}
+
+int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram, void* d_ws,
+                        size_t ws_bytes, hipStream_t st) {
+  if (N <= 0) return SYSID_OK;
+  if (d_ws == nullptr || ws_bytes < gram_ws_bytes(e, N))
+    return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, gram_ws_bytes(e, N));
+  const int64_t C = gram_chunk(e, N), rows0 = C * e->nv;
+  double* panel = static_cast<double*>(d_ws);
+  double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + align256((size_t)rows0 * e->ldp * sizeof(double)));
+  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows0));
+  const int ks0 = ksplit_for(e, rows0);
+  int rc;
+  for (int64_t c0 = 0; c0 < N; c0 += C) {
+    const int64_t n = std::min(C, N - c0);
+    if ((rc = launch_k1(e, d_in + c0, n, ld, panel, e->ldp, st, nullptr)) != SYSID_OK) return rc;
+    const int ks = std::min(ks0, ksplit_for(e, n * e->nv));
+    if ((rc = launch_k2(e, panel, n * e->nv, e->ldp, ks, c0 > 0, slab, st)) != SYSID_OK) return rc;
+  }
+  return launch_k3(e, ks0, slab, part, d_gram, st);
+}
+
 }  // namespace
 
 extern "C" {
 
-int32_t sysid_abi_version(void) { return 2; }
+int32_t sysid_abi_version(void) { return 3; }
 
 const char* sysid_last_error(const sysid_engine* e) { return e ? e->err.c_str() : g_thread_error.c_str(); }
 
@@ -465,6 +510,25 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
   return launch_stages(e, d_in, N, ld, flags, d_panel, ld_panel, d_gram, d_ws, ws_bytes, st, nullptr);
 }
 
+size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N) {
+  if (!e || N <= 0) return 0;
+  return gram_ws_bytes(e, N);
+}
+
+int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram,
+                                void* d_ws, size_t ws_bytes, void* stream) {
+  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
+  if (N < 0 || ld < N || (N > 0 && !d_in) || !d_gram)
+    return set_err(e, SYSID_E_INVALID, "bad arguments (N=%lld ld=%lld)", (long long)N, (long long)ld);
+  HIP_TRY(e, hipSetDevice(e->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (N == 0) {
+    HIP_TRY(e, hipMemsetAsync(d_gram, 0, (size_t)e->ncol * e->ncol * sizeof(double), st));
+    return SYSID_OK;
+  }
+  return launch_gram_chunked(e, d_in, N, ld, d_gram, d_ws, ws_bytes, st);
+}
+
 int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                           int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, int32_t iters, double* ms) {
   if (!e || !ms || iters <= 0) return set_err(e, SYSID_E_INVALID, "bad arguments");
@@ -510,12 +574,17 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     return SYSID_OK;
   }
   const int64_t rows = N * e->nv;
+  // no stacked output requested: Gram-only, the panel is produced chunk by chunk on the device
+  const bool panel_out = ((flags & SYSID_EMIT_Y) && Y_proj) || ((flags & SYSID_EMIT_TAU) && tau_proj) ||
+                         ((flags & SYSID_EMIT_FRICTION) && (B_v || B_c) && e->nj);
+  const bool gram_only = want_gram && !panel_out;
   int rc;
   if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) return rc;
-  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
+  if (!gram_only &&
+      (rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
     return rc;
   if (!e->d_gram) HIP_TRY(e, hipMalloc(&e->d_gram, (size_t)e->ncol * e->ncol * sizeof(double)));
-  const size_t wsb = sysid_workspace_bytes(e, N, flags);
+  const size_t wsb = gram_only ? gram_ws_bytes(e, N) : sysid_workspace_bytes(e, N, flags);
   if ((rc = grow(e, &e->d_ws, &e->ws_cap, wsb ? wsb : 256))) return rc;
   hipStream_t st = e->stream;
   const size_t rowb = (size_t)N * sizeof(double);
@@ -528,7 +597,8 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
                                   hipMemcpyHostToDevice, st));
     r0 += nrows[k];
   }
-  rc = launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
+  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, e->d_gram, e->d_ws, e->ws_cap, st)
+                 : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
   if (rc != SYSID_OK) return rc;
   const size_t pitch = (size_t)e->ldp * sizeof(double);
   if (Y_proj && (flags & SYSID_EMIT_Y))

@@ -698,7 +698,7 @@ __host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) /
 template <int NTC, int KC>
 __global__ void __launch_bounds__(64 * K2_WAVES)
 k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
-             int ngroups, int ksplit, int nslots, double* __restrict__ slab) {
+             int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;                       // doubles per LDS buffer
   constexpr int NT = 64 * K2_WAVES;
@@ -797,7 +797,10 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
     for (int t = 0; t < 4; ++t) {
       double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[((lane >> 4) + 4 * j) * 16 + (lane & 15)] = acc[s][t][j];
+      for (int j = 0; j < 4; ++j) {
+        double* x = o + ((lane >> 4) + 4 * j) * 16 + (lane & 15);
+        *x = accumulate ? *x + acc[s][t][j] : acc[s][t][j];  // chunked Gram: slabs carry over chunks
+      }
     }
   }
 }

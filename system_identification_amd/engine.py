@@ -52,6 +52,8 @@ SIGNATURES = [
     ("sysid_debug_k1_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
+    ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
+    ("sysid_build_gram_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _c.c_size_t, _vp]),
 ]
 
 _LIB = None
@@ -198,6 +200,30 @@ class Engine:
         rc = self.lib.sysid_build_device(
             self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(ld), int(flags),
             ctypes.c_void_p(bufs["panel"].data_ptr()), int(bufs["panel"].stride(0)),
+            ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
+            int(bufs["ws"].numel()), ctypes.c_void_p(st))
+        self._check(rc)
+
+    # ---- Gram-only device path (panel produced chunk by chunk inside the workspace) -------------
+    def gram_workspace_bytes(self, N: int) -> int:
+        return int(self.lib.sysid_gram_workspace_bytes(self._h, int(N)))
+
+    def alloc_gram_device(self, N: int) -> dict:
+        import torch
+        dev = torch.device("cuda", self.device)
+        return {
+            "gram": torch.empty((self.panel_cols, self.panel_cols), dtype=torch.float64, device=dev),
+            "ws": torch.empty(max(self.gram_workspace_bytes(N), 256), dtype=torch.uint8, device=dev),
+        }
+
+    def build_gram_device(self, d_in, N: int, bufs: dict, stream=None):
+        """Normal equations of N samples without materialising the N·nv-row panel (stream-ordered)."""
+        import torch
+        if d_in.dtype != torch.float64 or not d_in.is_cuda or d_in.shape[0] != self.in_rows:
+            raise ValueError(f"d_in must be a float64 CUDA tensor with {self.in_rows} channel rows")
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.lib.sysid_build_gram_device(
+            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)),
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)

@@ -164,6 +164,35 @@ def test_full_size_properties(robot, N):
         assert rel(rows, A) < TOL
 
 
+@pytest.mark.parametrize("robot,N", [("spot", 50000), ("g1_29dof", 12000)])
+def test_gram_only_chunked(robot, N):
+    """Gram-only path (panel produced in ~512 MiB chunks on the device, several chunks here) against
+    the full-panel path, on the host API and on the device API; bitwise repeatable."""
+    import torch
+    model = load_robot(robot)
+    e = eng(robot)
+    d = generate(model, N, config_index=3)
+    full = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_ALL)
+    only = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_GRAM)
+    assert set(only) == {"gram", "Atb", "btb", "num_rows"}
+    assert rel(only["gram"], full["gram"]) < 1e-12
+    assert rel(only["Atb"], full["Atb"]) < 1e-12
+    assert abs(only["btb"] - full["btb"]) <= 1e-12 * abs(full["btb"])
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_gram_device(N)
+    e.build_gram_device(din, N, bufs)
+    torch.cuda.synchronize()
+    G1 = bufs["gram"].clone()
+    assert np.array_equal(G1[:e.w, :e.w].cpu().numpy(), only["gram"])
+    e.build_gram_device(din, N, bufs)
+    torch.cuda.synchronize()
+    assert torch.equal(G1, bufs["gram"])
+    # too small a workspace is rejected, not overrun
+    small = {"gram": bufs["gram"], "ws": bufs["ws"][:1024]}
+    with pytest.raises(ValueError):
+        e.build_gram_device(din, N, small)
+
+
 def test_sysid_api_and_demo_functions():
     from system_identification_amd.demo import get_projected_friction_regressors, get_projected_y_tau
     from system_identification_amd.sys_identification import SystemIdentification
