@@ -133,7 +133,8 @@ int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_
  * of pinocchio's bodyRegressor(v, a_gf) moved to the world frame.  Used by the CPU test-suite. */
 int32_t sysid_debug_body_column(const double* body24, int32_t p, double* fw6);
 /* LDS image of K1 for one sample (inputs as in sysid_build with N = ld = 1) after the projector / H1
- * phases; sysid_debug_layout gives the offsets {in, body, W, Pt, Jw, pf, Jc(=Q), M(=L), P, H1, tp, total}. */
+ * phases; sysid_debug_layout gives the offsets {in, body, W, Pt, Jw, pf, Jc, M(=X, two buffers), P, H1, tp,
+ * total} (W/Pt/pf share their space with Z = X J_c). */
 int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq,
                         const double* tau, const double* cnt, double* lds_image, int64_t image_doubles);
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12);

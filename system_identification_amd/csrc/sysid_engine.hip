@@ -368,7 +368,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
   kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL.total; kp.out_cols = e->ldp;
-  kp.rg = std::max(1, 64 / std::max(1, NJ - 1));
+  kp.rg = k1_row_groups(NJ);
   kp.thr_rel = 1e-13;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;

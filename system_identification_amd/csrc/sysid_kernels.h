@@ -57,9 +57,16 @@ __host__ __device__ inline MImg mimg_layout(int NJ, int nv, int nc, int maxch) {
   return m;
 }
 
-// Per-wave LDS region of K1 (doubles, every piece 16-B aligned).
+// Row groups of K1's regressor-column phase: lanes = bodies x row groups, one pass of 64 lanes.
+__host__ __device__ inline int k1_row_groups(int NJ) {
+  const int nb = NJ - 1 > 0 ? NJ - 1 : 1;
+  return 64 / nb > 1 ? 64 / nb : 1;
+}
+
+// Per-wave LDS region of K1 (doubles, every piece 16-B aligned).  W, Pt, pf (dead once J_c is built)
+// and Z (dead once P is built) share one region.
 struct WLay {
-  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, total;
+  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, Z, total;
 };
 
 __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc) {
@@ -69,15 +76,19 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc)
   auto take = [&](int n) { const int r = o; o += (n + 1) & ~1; return r; };
   l.in = take(in_rows);
   l.body = take(NJ * 24);       // per joint: oR(9) ot(3) v(6) a_gf(6)
-  l.W = take(nv * 3);           // world direction of every dof's motion axis
-  l.Pt = take(nv * 3);          // a point on it
-  l.Jw = take(nv * 6);          // world spatial axis [linear at origin; angular]
-  l.pf = take(nc * 3);          // contact points (world)
-  l.Jc = take(k * nv);          // J_c, then Q = L^-1 J_c in place
-  l.M = take(k * k);            // J_c J_c^T, then its Cholesky factor in place
-  l.P = take(nv * nv);          // P = I - Q^T Q
+  l.Jw = take(nv * 6);          // spatial axis of every dof [linear at origin; angular]
   l.H1 = take(nv * 6);          // P[:, ff] J_w[:, ff]^T
   l.tp = take(nv);              // P S^T tau
+  const int u0 = o;
+  l.W = take(nv * 3);           // direction of every dof's motion axis
+  l.Pt = take(nv * 3);          // a point on it
+  l.pf = take(nc * 3);          // contact points
+  l.Z = u0;                     // Z = X J_c
+  const int zend = u0 + ((k * nv + 1) & ~1);
+  if (o < zend) o = zend;
+  l.Jc = take(k * nv);          // J_c
+  l.M = take(2 * k * k);        // J_c J_c^T, then X = its inverse (two exchange buffers)
+  l.P = take(nv * nv);          // P = I - J_c^T X J_c
   l.total = o;
   return l;
 }
@@ -86,7 +97,7 @@ struct K1Params {
   int nq, nv, NJ, nc, bd, nj, maxdepth, wy, w, ncol, in_rows, maxch, has_ff, ff0, mimg_dbl, wave_dbl;
   int out_cols;     // columns written per panel row (ncol rounded up to the panel's even stride)
   int rg;           // row groups of the regressor-column phase (lanes = bodies x rg)
-  double thr_rel;   // Cholesky pivot cut (relative to max diag(J_c J_c^T))
+  double thr_rel;   // pivot cut of the J_c J_c^T inversion (relative to its max diagonal)
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
 };
 
@@ -512,47 +523,67 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     K1_STAMP(3)
 
-    // ---- in-place Cholesky of M (right-looking); pivots <= thr_rel * max diag are dropped ----
+    // ---- X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, ping-ponging between two LDS buffers ----
+    // One pivot per step (no square roots, one reciprocal); every entry of a step reads only the
+    // previous buffer, so each step is a single wave-synchronous pass.  A pivot <= thr_rel * max diag
+    // (a contact row dependent on the kept ones) is dropped: ip = 0 zeroes its row and column and
+    // leaves the rest untouched, i.e. X is the inverse on the kept rows, as pinv treats them.
+    const double* Xs = Ms;
     {
       double dmax = 0.0;
       for (int a = 0; a < k; ++a) dmax = fmax(dmax, Ms[a * k + a]);
       const double thr = kp.thr_rel * dmax;
+      const float rk = k > 0 ? 1.0f / (float)k : 0.0f;
+      double* src = Ms;
+      double* dst = Ms + k * k;
       for (int j = 0; j < k; ++j) {
-        const double djj = Ms[j * k + j];
-        wsync();
-        const bool keep = djj > thr;
-        const double ljj = keep ? sqrt(djj) : 0.0;
-        for (int i = j + lane; i < k; i += 64)
-          Ms[i * k + j] = !keep ? 0.0 : (i == j ? ljj : Ms[i * k + j] / ljj);
-        wsync();
-        const int rem = k - j - 1;
-        for (int e = lane; e < rem * rem; e += 64) {
-          const int i = j + 1 + e / rem, l = j + 1 + e % rem;
-          if (l <= i) Ms[i * k + l] -= Ms[i * k + j] * Ms[l * k + j];
+        const double pj = src[j * k + j];
+        // three entries per lane per pass: all their loads issue before any store of the pass
+        for (int e0 = lane; e0 < k * k; e0 += 192) {
+          int r[3], c[3];
+          double arc[3], arj[3], ajc[3];
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int e = e0 + 64 * u;
+            const int ee = e < k * k ? e : 0;
+            r[u] = (int)(((float)ee + 0.5f) * rk);  // exact: ee < 24*24
+            c[u] = ee - r[u] * k;
+            arc[u] = src[ee];
+            arj[u] = src[r[u] * k + j];
+            ajc[u] = src[j * k + c[u]];
+          }
+          const double ip = pj > thr ? 1.0 / pj : 0.0;
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const double v = r[u] == j ? (c[u] == j ? ip : ajc[u] * ip)
+                                       : (c[u] == j ? -arj[u] * ip : arc[u] - arj[u] * ajc[u] * ip);
+            if (e0 + 64 * u < k * k) dst[e0 + 64 * u] = v;
+          }
         }
         wsync();
+        double* t = src;
+        src = dst;
+        dst = t;
       }
+      Xs = src;
     }
     K1_STAMP(4)
 
-    // ---- Q = L^-1 J_c (one column per lane, in place) ----
-    for (int r = lane; r < nv; r += 64) {
-      for (int j = 0; j < k; ++j) {
-        const double ljj = Ms[j * k + j];
-        double x = Jc[j * nv + r];
+    // ---- Z = X J_c ;  P = I - J_c^T Z ----
+    double* Zs = wr + L.Z;
+    for (int e = lane; e < k * nv; e += 64) {
+      const int a = e / nv, r = e - a * nv;
+      double acc = 0.0;
 #pragma unroll 4
-        for (int l = 0; l < j; ++l) x -= Ms[j * k + l] * Jc[l * nv + r];
-        Jc[j * nv + r] = ljj != 0.0 ? x / ljj : 0.0;
-      }
+      for (int b = 0; b < k; ++b) acc += Xs[a * k + b] * Jc[b * nv + r];
+      Zs[e] = acc;
     }
     wsync();
-
-    // ---- P = I - Q^T Q ----
     for (int e = lane; e < nv * nv; e += 64) {
       const int a = e / nv, b = e - a * nv;
       double acc = 0.0;
 #pragma unroll 4
-      for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Jc[j * nv + b];
+      for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Zs[j * nv + b];
       Ps[e] = (a == b ? 1.0 : 0.0) - acc;
     }
     wsync();
@@ -585,7 +616,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
-    // One G row (6 + 6*chain FMAs) feeds 42 FMAs and five 16-byte stores.
+    // One G row (6 + 6*chain FMAs) feeds 42 FMAs and five 16-byte stores.  (Staging the rows through
+    // LDS to make the stores contiguous measured 17% slower: the store path is not the limiter.)
     double* out = panel + (s * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
     for (int it = lane; it < nyi; it += 64) {

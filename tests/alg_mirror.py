@@ -36,7 +36,9 @@ def world_axes(model, d):
     return W, Pt, lin
 
 
-def projector_cholqr(model, d, cnt, W, Pt, lin, tol=1e-12):
+def projector_exchange(model, d, cnt, W, Pt, lin, thr_rel=1e-13):
+    """P = I - J_c^T X J_c with X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, pivots <= thr_rel * max diag
+    dropped (their row and column of X zeroed), as K1 computes it."""
     rows = []
     for k, f in enumerate(model.contact_frames()):
         if not cnt[k]:
@@ -50,24 +52,19 @@ def projector_cholqr(model, d, cnt, W, Pt, lin, tol=1e-12):
     if not rows:
         return np.eye(nv)
     Jc = np.vstack(rows)
-    M = Jc @ Jc.T
-    k = M.shape[0]
-    L = np.zeros((k, k))
-    keep = np.ones(k, dtype=bool)
-    dmax = max(np.max(np.diag(M)), 1e-300)
+    X = Jc @ Jc.T
+    k = X.shape[0]
+    thr = thr_rel * np.max(np.diag(X))
     for j in range(k):
-        s = M[j, j] - L[j, :j] @ L[j, :j]
-        if s <= tol * dmax:
-            keep[j] = False
-            continue
-        L[j, j] = np.sqrt(s)
-        for i in range(j + 1, k):
-            L[i, j] = (M[i, j] - L[i, :j] @ L[j, :j]) / L[j, j]
-    Q = np.zeros((k, nv))
-    for j in range(k):
-        if keep[j]:
-            Q[j] = (Jc[j] - L[j, :j] @ Q[:j]) / L[j, j]
-    return np.eye(nv) - Q.T @ Q
+        p = X[j, j]
+        ip = 1.0 / p if p > thr else 0.0
+        Y = X - np.outer(X[:, j], X[j, :]) * ip
+        Y[j, :] = X[j, :] * ip
+        Y[:, j] = -X[:, j] * ip
+        Y[j, j] = ip
+        X = Y
+    Z = X @ Jc
+    return np.eye(nv) - Jc.T @ Z
 
 
 def base_relative(model, d):
@@ -86,7 +83,7 @@ def sample_panel(model, q, dq, ddq, tau, cnt):
     """[Y_proj | B_v | B_c | tau_proj] for one sample via the kernel formulation."""
     d = base_relative(model, ref.forward_pass(model, q, dq, ddq))
     W, Pt, lin = world_axes(model, d)
-    P = projector_cholqr(model, d, cnt, W, Pt, lin)
+    P = projector_exchange(model, d, cnt, W, Pt, lin)
     nv, nb = model.nv, model.nb
     Jw = np.zeros((6, nv))  # world spatial axes [linear at origin; angular]
     for r in range(nv):

@@ -42,14 +42,14 @@ def test_c_oracle_matches_golden(robot):
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_kernel_formulation_matches_golden(robot):
-    """The HIP kernel's algebra (world axes, Cholesky-QR projector, H1 + revolute chain) in numpy."""
+    """The HIP kernel's algebra (world axes, exchange-inverse projector, H1 + revolute chain) in numpy."""
     g, m = load(robot), load_robot(robot)
     nv = m.nv
     for s in range(g["q"].shape[1]):
         Y, t, Bv, Bc = am.sample_panel(m, g["q"][:, s], g["dq"][:, s], g["ddq"][:, s], g["tau"][:, s], g["contact"][:, s])
         sl = slice(s * nv, (s + 1) * nv)
         for a, b in ((Y, g["Y_proj"][sl]), (t, g["tau_proj"][sl]), (Bv, g["B_v"][sl]), (Bc, g["B_c"][sl])):
-            assert rel(a, b) < 1e-6  # north_star parity bar; Cholesky-QR projector error ~ eps·cond(J_c)^2
+            assert rel(a, b) < 1e-6  # north_star parity bar; (J_c J_c^T)^-1 projector error ~ eps·cond(J_c)^2
 
 
 @pytest.mark.parametrize("robot", ROBOTS)
