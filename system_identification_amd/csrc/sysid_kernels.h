@@ -778,10 +778,16 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
   // fragment columns of this wave: f = 4*s + {I0, I0+1, J0, J0+1} (16-column blocks)
   int foff[4 * K2_SPW];
   bool live[K2_SPW];
+  bool need[K2_SPW][4];  // wave-uniform: skip the lower tile of a diagonal super-tile, tiles past NTC
 #pragma unroll
   for (int s = 0; s < K2_SPW; ++s) {
     const int2 sp = supers[sbase + s];
     live[s] = sp.x >= 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int I = 2 * sp.x + (t >> 1), J = 2 * sp.y + (t & 1);
+      need[s][t] = live[s] && I <= J && J < NTC;
+    }
     const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -812,10 +818,10 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
       for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = cur[foff[u] + kk * STRIDE];
 #pragma unroll
       for (int s = 0; s < K2_SPW; ++s) {
-        acc[s][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 2], acc[s][0], 0, 0, 0);
-        acc[s][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 3], acc[s][1], 0, 0, 0);
-        acc[s][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 2], acc[s][2], 0, 0, 0);
-        acc[s][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 3], acc[s][3], 0, 0, 0);
+        if (need[s][0]) acc[s][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 2], acc[s][0], 0, 0, 0);
+        if (need[s][1]) acc[s][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 3], acc[s][1], 0, 0, 0);
+        if (need[s][2]) acc[s][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 2], acc[s][2], 0, 0, 0);
+        if (need[s][3]) acc[s][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 3], acc[s][3], 0, 0, 0);
       }
     }
     if (c + 1 < nchunks) store_chunk(lds + ((c + 1) & 1) * BUF);
