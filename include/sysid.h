@@ -116,10 +116,34 @@ size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N);
 int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram,
                                 void* d_workspace, size_t workspace_bytes, void* stream);
 
+/* Torque-prediction errors: print_tau_prediction_rmse
+ * (src/sys_identification.py:421-437) as one reduction over the stacked panel instead of a second
+ * per-sample pass.  err_sq[d] = sum over samples of (Y_proj[s·nv+d, :]·phi − tau_proj[s·nv+d])², for all nv
+ * rows d (the reference reports d >= 6: total = sum(err_sq[6:]) / N, per joint sqrt(err_sq[6+j] / N)).
+ * phi: 10·nb inertial parameters (pinocchio order).  Deterministic (fixed reduction order).
+ * Host form: builds the panel on the device (never copied back) and returns err_sq (nv doubles).
+ * Device form: d_panel as written by sysid_build_device, d_phi/d_err_sq device buffers. */
+int32_t sysid_tau_error(sysid_engine* e, const double* q, const double* dq, const double* ddq,
+                        const double* tau, const double* cnt, int64_t N, int64_t ld, const double* phi,
+                        double* err_sq);
+size_t sysid_tau_error_workspace_bytes(const sysid_engine* e, int64_t N);
+int32_t sysid_tau_error_device(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t N,
+                               const double* d_phi, double* d_err_sq, void* d_workspace,
+                               size_t workspace_bytes, void* stream);
+
 /* Host-side check of the contact contract for n_contact x ld contact values (SYSID_E_CONTACT on the
  * first offending sample, whose index is written to *bad_sample when non-NULL). */
 int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld,
                              int64_t* bad_sample);
+
+/* Ingest: native reader of the reference's .dat logs (read_data,
+ * demo/spot_identification.py:9-14): tab-delimited text, one channel per line, parsed like
+ * np.loadtxt(path, delimiter='\t', dtype=np.float32) (field -> double, correctly rounded -> float32),
+ * in parallel over spans of each line.  Host-only; no device needed.  Errors: SYSID_E_INVALID with
+ * sysid_io_last_error() (per thread). */
+int32_t sysid_dat_shape(const char* path, int64_t* rows, int64_t* cols);
+int32_t sysid_dat_read(const char* path, float* out, int64_t rows, int64_t cols, int32_t nthreads);
+const char* sysid_io_last_error(void);
 
 /* Kernel-only timing helper for bench.py: runs sysid_build_device `iters` times on the engine's
  * stream bracketed by HIP events and returns the mean milliseconds per kernel of each stage:

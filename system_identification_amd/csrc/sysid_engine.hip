@@ -248,6 +248,25 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   return launch_k3(e, ks0, slab, part, d_gram, st);
 }
 
+int k4_blocks(const sysid_engine* e, int64_t N) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)e->cus * 4, N));
+}
+
+int launch_k4(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t N, const double* d_phi,
+              double* d_err_sq, void* d_ws, size_t ws_bytes, hipStream_t st) {
+  const int nb = k4_blocks(e, N);
+  if (d_ws == nullptr || ws_bytes < (size_t)nb * e->nv * sizeof(double))
+    return set_err(e, SYSID_E_INVALID, "workspace too small for the torque-error reduction");
+  if (e->wy > K4_MAXWY) return set_err(e, SYSID_E_MODEL, "regressor width %d > %d", e->wy, K4_MAXWY);
+  double* part = static_cast<double*>(d_ws);
+  hipLaunchKernelGGL(k4_tau_error, dim3((unsigned)nb), dim3(256), 0, st, d_panel, ld_panel, N, e->nv, e->wy, e->w,
+                     d_phi, part);
+  HIP_TRY(e, hipGetLastError());
+  hipLaunchKernelGGL(k4_tau_error_final, dim3(1), dim3(64), 0, st, part, nb, e->nv, d_err_sq);
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -530,6 +549,70 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
     return SYSID_OK;
   }
   return launch_gram_chunked(e, d_in, N, ld, d_gram, d_ws, ws_bytes, st);
+}
+
+size_t sysid_tau_error_workspace_bytes(const sysid_engine* e, int64_t N) {
+  if (!e) return 0;
+  return align256((size_t)k4_blocks(e, N) * e->nv * sizeof(double));
+}
+
+int32_t sysid_tau_error_device(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t N,
+                               const double* d_phi, double* d_err_sq, void* d_ws, size_t ws_bytes, void* stream) {
+  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
+  if (N < 0 || ld_panel < e->ncol || (ld_panel & 1) || !d_phi || !d_err_sq || (N > 0 && !d_panel) ||
+      (reinterpret_cast<uintptr_t>(d_panel) & 15))
+    return set_err(e, SYSID_E_INVALID, "bad arguments");
+  HIP_TRY(e, hipSetDevice(e->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (N == 0) {
+    HIP_TRY(e, hipMemsetAsync(d_err_sq, 0, (size_t)e->nv * sizeof(double), st));
+    return SYSID_OK;
+  }
+  return launch_k4(e, d_panel, ld_panel, N, d_phi, d_err_sq, d_ws, ws_bytes, st);
+}
+
+int32_t sysid_tau_error(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
+                        const double* cnt, int64_t N, int64_t ld, const double* phi, double* err_sq) {
+  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
+  if (N < 0 || ld < N || !phi || !err_sq) return set_err(e, SYSID_E_INVALID, "bad arguments");
+  if (N > 0 && (!q || !dq || !ddq || (!tau && e->nj) || (!cnt && e->nc)))
+    return set_err(e, SYSID_E_INVALID, "null input buffer");
+  if (N == 0) {
+    std::memset(err_sq, 0, (size_t)e->nv * sizeof(double));
+    return SYSID_OK;
+  }
+  if (e->nc) {
+    const int rc = sysid_check_contacts(e, cnt, N, ld, nullptr);
+    if (rc != SYSID_OK) return rc;
+  }
+  HIP_TRY(e, hipSetDevice(e->device));
+  const int64_t rows = N * e->nv;
+  int rc;
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) return rc;
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
+    return rc;
+  const size_t wsb = sysid_tau_error_workspace_bytes(e, N) + align256((size_t)(e->wy + e->nv) * sizeof(double));
+  if ((rc = grow(e, &e->d_ws, &e->ws_cap, wsb))) return rc;
+  hipStream_t st = e->stream;
+  const size_t rowb = (size_t)N * sizeof(double);
+  const double* srcs[5] = {q, dq, ddq, tau, cnt};
+  const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
+  int64_t r0 = 0;
+  for (int k = 0; k < 5; ++k) {
+    if (nrows[k] > 0)
+      HIP_TRY(e, hipMemcpy2DAsync(e->d_in + r0 * N, rowb, srcs[k], (size_t)ld * sizeof(double), rowb, nrows[k],
+                                  hipMemcpyHostToDevice, st));
+    r0 += nrows[k];
+  }
+  double* d_phi = reinterpret_cast<double*>(static_cast<char*>(e->d_ws) + sysid_tau_error_workspace_bytes(e, N));
+  double* d_err = d_phi + e->wy;
+  HIP_TRY(e, hipMemcpyAsync(d_phi, phi, (size_t)e->wy * sizeof(double), hipMemcpyHostToDevice, st));
+  if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, st, nullptr)) != SYSID_OK) return rc;
+  if ((rc = launch_k4(e, e->d_panel, e->ldp, N, d_phi, d_err, e->d_ws, sysid_tau_error_workspace_bytes(e, N), st)))
+    return rc;
+  HIP_TRY(e, hipMemcpyAsync(err_sq, d_err, (size_t)e->nv * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIP_TRY(e, hipStreamSynchronize(st));
+  return SYSID_OK;
 }
 
 int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,

@@ -881,6 +881,58 @@ k3_gram_final(const double* __restrict__ part, const int2* __restrict__ tiles, i
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// K4: torque-prediction errors of the stacked system (print_tau_prediction_rmse,
+// src/sys_identification.py:421-437, without its second pass over the samples):
+//   e[s, d] = Y_proj[s*nv + d, :] . phi - tau_proj[s*nv + d];   part[block][d] = sum over its samples e^2.
+// Thread t of a block owns dof d = t % nv of samples t / nv, t / nv + spb, ... (spb = 256 / nv), so
+// every thread accumulates one dof and the block sum per dof runs in a fixed order: deterministic.
+// HBM-bound (reads the Y_proj and tau columns once).
+// ------------------------------------------------------------------------------------------------
+constexpr int K4_MAXWY = 640;
+
+__global__ void __launch_bounds__(256)
+k4_tau_error(const double* __restrict__ panel, int64_t ldp, int64_t N, int nv, int wy, int w,
+             const double* __restrict__ phi, double* __restrict__ part) {
+  __shared__ double sphi[K4_MAXWY];
+  __shared__ double red[256];
+  for (int c = threadIdx.x; c < wy; c += 256) sphi[c] = phi[c];
+  __syncthreads();
+  const int spb = 256 / nv, t = threadIdx.x, so = t / nv, d = t - so * nv;
+  const int64_t s0 = (int64_t)blockIdx.x * N / gridDim.x, s1 = (int64_t)(blockIdx.x + 1) * N / gridDim.x;
+  double acc = 0.0;
+  if (so < spb) {
+    for (int64_t s = s0 + so; s < s1; s += spb) {
+      const double* row = panel + (s * nv + d) * ldp;
+      const double2* row2 = reinterpret_cast<const double2*>(row);
+      double a0 = 0.0, a1 = 0.0;
+      for (int c = 0; c < (wy >> 1); ++c) {
+        const double2 v = row2[c];
+        a0 += v.x * sphi[2 * c];
+        a1 += v.y * sphi[2 * c + 1];
+      }
+      const double e = (a0 + a1) - row[w];
+      acc += e * e;
+    }
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (t < nv) {
+    double sum = 0.0;
+    for (int u = 0; u < spb; ++u) sum += red[u * nv + t];
+    part[(int64_t)blockIdx.x * nv + t] = sum;
+  }
+}
+
+__global__ void __launch_bounds__(64)
+k4_tau_error_final(const double* __restrict__ part, int nblocks, int nv, double* __restrict__ err_sq) {
+  for (int d = threadIdx.x; d < nv; d += 64) {
+    double sum = 0.0;
+    for (int b = 0; b < nblocks; ++b) sum += part[(int64_t)b * nv + d];
+    err_sq[d] = sum;
+  }
+}
+
 // Diagnostics kernel: lane l computes column (l % 10) of the body regressor in world frame.
 __global__ void debug_body_column_kernel(const double* __restrict__ body24, double* __restrict__ out) {
   __shared__ double b[24];

@@ -27,16 +27,34 @@ def write_dat(path: str, robot_name: str, data: dict) -> None:
         np.savetxt(dat_path(path, robot_name, ch), np.atleast_2d(a), delimiter="\t", fmt="%.9g")
 
 
+def load_dat(filename: str, nthreads: int = 0) -> np.ndarray:
+    """np.loadtxt(filename, delimiter='\\t', dtype=np.float32) through the native parallel parser in libsysid.so
+    (bit-identical values; same squeeze of unit dimensions as loadtxt's default ndmin=0)."""
+    import ctypes
+    from .engine import load_library
+    lib = load_library()
+    fn = os.fsencode(str(filename))
+    rows, cols = ctypes.c_int64(), ctypes.c_int64()
+    if lib.sysid_dat_shape(fn, ctypes.byref(rows), ctypes.byref(cols)) != 0:
+        raise ValueError(lib.sysid_io_last_error().decode())
+    out = np.empty((rows.value, cols.value), dtype=np.float32)
+    ptr = out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    if lib.sysid_dat_read(fn, ptr, rows.value, cols.value, int(nthreads)) != 0:
+        raise ValueError(lib.sysid_io_last_error().decode())
+    return np.squeeze(out) if 1 in out.shape else out
+
+
 def read_data(path, robot_name, filter_type):
-    """demo/spot_identification.py:9-34 (solo's variant :9-33 is this with robot_name="solo")."""
+    """demo/spot_identification.py:9-34 (solo's variant :9-33 is this with robot_name="solo").  The five
+    files are parsed natively (load_dat); the filters are the reference's scipy calls, on the host."""
     import scipy.signal as signal
     from scipy.signal import savgol_filter
     path = str(path)
-    q = np.loadtxt(dat_path(path, robot_name, "q"), delimiter="\t", dtype=np.float32)
-    dq = np.loadtxt(dat_path(path, robot_name, "dq"), delimiter="\t", dtype=np.float32)
-    ddq = np.loadtxt(dat_path(path, robot_name, "ddq"), delimiter="\t", dtype=np.float32)
-    tau = np.loadtxt(dat_path(path, robot_name, "tau"), delimiter="\t", dtype=np.float32)
-    cnt = np.loadtxt(dat_path(path, robot_name, "contact"), delimiter="\t", dtype=np.float32)
+    q = load_dat(dat_path(path, robot_name, "q"))
+    dq = load_dat(dat_path(path, robot_name, "dq"))
+    ddq = load_dat(dat_path(path, robot_name, "ddq"))
+    tau = load_dat(dat_path(path, robot_name, "tau"))
+    cnt = load_dat(dat_path(path, robot_name, "contact"))
     if filter_type == "butterworth":
         b, a = signal.butter(5, 0.15, btype="low", analog=False)
         dq = signal.filtfilt(b, a, dq, axis=1)

@@ -53,6 +53,12 @@ SIGNATURES = [
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
+    ("sysid_dat_shape", _c.c_int32, [_c.c_char_p, _c.POINTER(_c.c_int64), _c.POINTER(_c.c_int64)]),
+    ("sysid_dat_read", _c.c_int32, [_c.c_char_p, _c.POINTER(_c.c_float), _c.c_int64, _c.c_int64, _c.c_int32]),
+    ("sysid_io_last_error", _c.c_char_p, []),
+    ("sysid_tau_error", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _dp, _dp]),
+    ("sysid_tau_error_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
+    ("sysid_tau_error_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _vp, _c.c_size_t, _vp]),
     ("sysid_build_gram_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _c.c_size_t, _vp]),
 ]
 
@@ -175,6 +181,37 @@ class Engine:
         if G is not None:
             out["gram"], out["Atb"], out["btb"], out["num_rows"] = G, g, float(btb[0]), R
         return out
+
+    def tau_error(self, q, dq, ddq, tau, cnt, phi) -> np.ndarray:
+        """Sum over samples of the squared torque-prediction error of every row (nv,), K4 on the device."""
+        ins = []
+        for a, rows, name in ((q, self.nq, "q"), (dq, self.nv, "dq"), (ddq, self.nv, "ddq"),
+                              (tau, self.nj, "tau"), (cnt, self.n_contact, "contact")):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+            if a.ndim == 1:
+                a = a.reshape(-1, 1)
+            if a.shape[0] != rows:
+                raise ValueError(f"{name}: expected {rows} channels, got shape {a.shape}")
+            ins.append(a)
+        N = ins[0].shape[1]
+        phi = np.ascontiguousarray(np.asarray(phi, dtype=np.float64).reshape(-1))
+        if phi.size != self.wy:
+            raise ValueError(f"phi: expected {self.wy} parameters, got {phi.size}")
+        err = np.zeros(self.nv)
+        self._check(self.lib.sysid_tau_error(self._h, *[_ptr(a) for a in ins], N, N, _ptr(phi), _ptr(err)))
+        return err
+
+    def tau_error_device(self, bufs: dict, N: int, d_phi, d_err, stream=None):
+        """K4 on a panel written by build_device; d_phi (10 nb,) and d_err (nv,) float64 CUDA tensors."""
+        import torch
+        ws = torch.empty(max(int(self.lib.sysid_tau_error_workspace_bytes(self._h, int(N))), 256),
+                         dtype=torch.uint8, device=bufs["panel"].device)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        self._check(self.lib.sysid_tau_error_device(
+            self._h, ctypes.c_void_p(bufs["panel"].data_ptr()), int(bufs["panel"].stride(0)), int(N),
+            ctypes.c_void_p(d_phi.data_ptr()), ctypes.c_void_p(d_err.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+            int(ws.numel()), ctypes.c_void_p(st)))
+        return ws  # keep alive until the stream has consumed it
 
     # ---- device-buffer path (torch tensors on this engine's device) ----------------------------
     def workspace_bytes(self, N: int, flags: int = EMIT_ALL) -> int:

@@ -84,13 +84,17 @@ class SystemIdentification(object):
         """Batched hot path.  Inputs channel-major (channels x N) as read_data returns them.
         Returns the stacked arrays the reference builds at demo/spot_identification.py:84-87
         (Y_proj, tau_proj, B_v, B_c) and, with EMIT_GRAM, the normal equations."""
+        ch = self._channels(q, dq, ddq, tau, cnt)  # shape errors before the device is touched
+        return self.engine.build(*ch, flags)
+
+    def _channels(self, q, dq, ddq, tau, cnt):
         m = self.model
         q = self._as_channels(q, m.nq, "q")
         dq = self._as_channels(dq, m.nv, "dq")
         ddq = self._as_channels(ddq, m.nv, "ddq")
         tau = self._as_channels(tau, m.nj, "tau") if m.nj else np.zeros((0, q.shape[1]))
         cnt = self._as_channels(cnt, m.n_ee, "contact") if m.n_ee else np.zeros((0, q.shape[1]))
-        return self.engine.build(q, dq, ddq, tau, cnt, flags)
+        return q, dq, ddq, tau, cnt
 
     def build_normal_equations(self, q, dq, ddq, tau, cnt) -> dict:
         """Gram of the stacked system: {gram: AᵀA, Atb: Aᵀb, btb: bᵀb, num_rows: N·nv} (src/solver.py:186-190)."""
@@ -212,11 +216,18 @@ class SystemIdentification(object):
         meas = out["tau_proj"].reshape(-1, nv)[:, bd:]
         return pred, meas
 
+    def tau_prediction_rmse(self, q, dq, ddq, torque, cnt, phi):
+        """(rmse_total, per-joint RMSE) of :432-433 from one device reduction (K4): the stacked panel is
+        built on the GPU and never copied back.  rmse_total keeps the reference's definition, the mean over
+        samples of the squared error norm."""
+        ch = self._channels(q, dq, ddq, torque, cnt)
+        N = ch[0].shape[1]
+        err = self.engine.tau_error(*ch, np.asarray(phi, dtype=np.float64))
+        bd = self._base_dof
+        return float(np.sum(err[bd:]) / N), np.sqrt(err[bd:] / N)
+
     def print_tau_prediction_rmse(self, q, dq, ddq, torque, cnt, phi, param_name):
-        tau_pred, tau_meas = self.tau_prediction_errors(q, dq, ddq, torque, cnt, phi)
-        error = tau_pred - tau_meas
-        rmse_total = np.mean(np.square(np.linalg.norm(error, axis=1)))
-        joint_tau_rmse = np.sqrt(np.mean(np.square(error), axis=0))
+        rmse_total, joint_tau_rmse = self.tau_prediction_rmse(q, dq, ddq, torque, cnt, phi)
         print("\n--------------------Torque Prediction Errors--------------------")
         print(f'RMSE for joint torques prediction using {param_name} parameters: total= {rmse_total}\n'
               f'per_joints={joint_tau_rmse}')

@@ -42,3 +42,33 @@ def test_dat_round_trip_and_filter(tmp_path):
     assert np.allclose(dq, signal.filtfilt(b, a, d["dq"].astype(np.float32), axis=1))
     q2, dq2, _, _, _ = read_data(str(tmp_path) + "/", "spot", "none")
     assert np.array_equal(dq2.astype(np.float64), d["dq"])
+
+
+def test_native_dat_reader_matches_loadtxt(tmp_path):
+    """sysid_dat_read (native, multi-threaded) is bit-identical to np.loadtxt(..., dtype=float32), the
+    reference's reader (demo/spot_identification.py:10-14), on awkward spellings, long rows split across
+    threads, a single-row file (loadtxt squeezes it to 1-D) and CRLF line ends; errors are ValueError."""
+    from system_identification_amd.datio import load_dat
+    rng = np.random.default_rng(7)
+    a = rng.standard_normal((5, 20011)) * 10.0 ** rng.integers(-8, 8, (5, 20011))
+    f = tmp_path / "x.dat"
+    np.savetxt(f, a, delimiter="\t", fmt="%.17g")  # full double text: exercises double->float32 rounding
+    ref = np.loadtxt(f, delimiter="\t", dtype=np.float32)
+    for nt in (1, 3, 16):
+        got = load_dat(f, nthreads=nt)
+        assert got.dtype == np.float32 and got.shape == ref.shape
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    g = tmp_path / "y.dat"
+    g.write_text("1\t-2.5e-3\t+7\tinf\t-inf\t1e40\t0.1\r\n\n3\t4\t5\t6\t7\t8\t9\r\n")
+    ref = np.loadtxt(g, delimiter="\t", dtype=np.float32)
+    got = load_dat(g)
+    assert np.array_equal(got, ref)
+    h = tmp_path / "one.dat"
+    h.write_text("0\t1\t2\t1\n")
+    assert np.array_equal(load_dat(h), np.loadtxt(h, delimiter="\t", dtype=np.float32))
+    bad = tmp_path / "bad.dat"
+    bad.write_text("1\t2\n3\n")
+    with pytest.raises(ValueError):
+        load_dat(bad)
+    with pytest.raises(ValueError):
+        load_dat(tmp_path / "missing.dat")
