@@ -136,6 +136,18 @@ int32_t sysid_tau_error_device(sysid_engine* e, const double* d_panel, int64_t l
 int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld,
                              int64_t* bad_sample);
 
+/* Multi-GPU exchange: one process per GPU, samples sharded, each rank builds its
+ * partial Gram, then one in-place sum all-reduce of the (W+1)x(W+1) fp64 Gram over RCCL/xGMI.
+ * RCCL is loaded at run time (the copy already in the process if any).  sysid_rccl_unique_id fills a
+ * 128-byte ncclUniqueId on one rank (distribute it out of band), sysid_rccl_comm_init creates the
+ * communicator of `rank` on `device`, sysid_allreduce_gram enqueues the reduction on `stream` (NULL = the
+ * device's null stream).  Errors: SYSID_E_DEVICE with sysid_rccl_last_error() (per thread). */
+int32_t sysid_rccl_unique_id(void* id128);
+int32_t sysid_rccl_comm_init(void** comm, int32_t nranks, const void* id128, int32_t rank, int32_t device);
+int32_t sysid_rccl_comm_destroy(void* comm);
+int32_t sysid_allreduce_gram(const sysid_engine* e, double* d_gram, void* comm, void* stream);
+const char* sysid_rccl_last_error(void);
+
 /* Ingest: native reader of the reference's .dat logs (read_data,
  * demo/spot_identification.py:9-14): tab-delimited text, one channel per line, parsed like
  * np.loadtxt(path, delimiter='\t', dtype=np.float32) (field -> double, correctly rounded -> float32),

@@ -72,3 +72,44 @@ def build_normal_equations_distributed(q, dq, ddq, tau, cnt, build_partial: Call
     if world == 1:
         return ne
     return allreduce_normal_equations(ne, device=device, group=group)
+
+
+class RcclGramComm:
+    """The C ABI's own exchange step (sysid_rccl_* / sysid_allreduce_gram): what a non-Python host would
+    call between its per-rank sysid_build_device and the solver.  The 128-byte unique id is created on
+    rank 0 and handed to the other ranks out of band (here: any callable, e.g. a torch.distributed or
+    file broadcast)."""
+
+    def __init__(self, engine, rank: int, world: int, share_id: Callable = None):
+        import ctypes
+        self.lib, self.engine = engine.lib, engine
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0 and self.lib.sysid_rccl_unique_id(uid) != 0:
+            raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
+        if world > 1:
+            if share_id is None:
+                raise ValueError("world > 1 needs share_id to distribute the RCCL unique id")
+            uid = ctypes.create_string_buffer(bytes(share_id(uid.raw)), 128)
+        self._comm = ctypes.c_void_p()
+        if self.lib.sysid_rccl_comm_init(ctypes.byref(self._comm), int(world), uid, int(rank), int(engine.device)) != 0:
+            raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
+
+    def allreduce_gram(self, gram, stream=None):
+        """In-place sum of a (W+1)x(W+1) float64 CUDA tensor over the ranks (stream-ordered)."""
+        import ctypes
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream(self.engine.device).cuda_stream
+        if self.lib.sysid_allreduce_gram(self.engine._h, ctypes.c_void_p(gram.data_ptr()), self._comm,
+                                         ctypes.c_void_p(st)) != 0:
+            raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
+
+    def close(self):
+        if getattr(self, "_comm", None) and self._comm.value:
+            self.lib.sysid_rccl_comm_destroy(self._comm)
+            self._comm = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

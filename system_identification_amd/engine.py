@@ -56,6 +56,11 @@ SIGNATURES = [
     ("sysid_dat_shape", _c.c_int32, [_c.c_char_p, _c.POINTER(_c.c_int64), _c.POINTER(_c.c_int64)]),
     ("sysid_dat_read", _c.c_int32, [_c.c_char_p, _c.POINTER(_c.c_float), _c.c_int64, _c.c_int64, _c.c_int32]),
     ("sysid_io_last_error", _c.c_char_p, []),
+    ("sysid_rccl_unique_id", _c.c_int32, [_vp]),
+    ("sysid_rccl_comm_init", _c.c_int32, [_c.POINTER(_vp), _c.c_int32, _vp, _c.c_int32, _c.c_int32]),
+    ("sysid_rccl_comm_destroy", _c.c_int32, [_vp]),
+    ("sysid_allreduce_gram", _c.c_int32, [_vp, _vp, _vp, _vp]),
+    ("sysid_rccl_last_error", _c.c_char_p, []),
     ("sysid_tau_error", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _dp, _dp]),
     ("sysid_tau_error_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
     ("sysid_tau_error_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _vp, _c.c_size_t, _vp]),

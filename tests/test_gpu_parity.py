@@ -226,6 +226,26 @@ def test_tau_prediction_rmse_reduction(robot, N):
         e.tau_error(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], phi[:-1])
 
 
+def test_rccl_gram_allreduce_single_rank():
+    """sysid_allreduce_gram over a one-rank RCCL communicator is the identity on the Gram (the N > 1 path
+    needs more GPUs than a test box has; its host logic is covered by the gloo tests)."""
+    import torch
+    from system_identification_amd.distributed import RcclGramComm
+    e = eng("spot")
+    N = 2000
+    d = generate(load_robot("spot"), N, config_index=6)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_gram_device(N)
+    e.build_gram_device(din, N, bufs)
+    torch.cuda.synchronize()
+    G0 = bufs["gram"].clone()
+    comm = RcclGramComm(e, rank=0, world=1)
+    comm.allreduce_gram(bufs["gram"])
+    torch.cuda.synchronize()
+    assert torch.equal(G0, bufs["gram"])
+    comm.close()
+
+
 def test_sysid_api_and_demo_functions():
     from system_identification_amd.demo import get_projected_friction_regressors, get_projected_y_tau
     from system_identification_amd.sys_identification import SystemIdentification
