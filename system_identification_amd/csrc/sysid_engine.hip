@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -448,6 +449,9 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       return SYSID_E_MODEL;
     }
     st = hipFuncSetAttribute(k1_fn(e->k1_variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
+#ifdef SYSID_EXPERIMENTS
+    if (const char* v = std::getenv("SYSID_K1_BLOCKS_PER_CU")) e->k1_blocks_per_cu = std::max(1, std::atoi(v));
+#endif
   }
   if (st != hipSuccess) {
     set_err(nullptr, SYSID_E_DEVICE, "device setup failed: %s", hipGetErrorString(st));
@@ -786,6 +790,25 @@ int32_t sysid_debug_stamps(sysid_engine* e, const double* d_in, int64_t N, int64
   (void)hipFree(e->d_dump);
   e->d_dump = nullptr;
   return rc;
+}
+#endif
+
+#ifdef SYSID_EXPERIMENTS
+// Experiments only: K2 (+K3 when final) on an existing panel, on a given stream.
+int32_t sysid_exp_k2(sysid_engine* e, const double* d_panel, int64_t N, int64_t ld_panel, int32_t accumulate,
+                     int32_t final, double* d_gram, void* d_ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t rows = N * e->nv;
+  const int ks = ksplit_for(e, rows);
+  double* slab = static_cast<double*>(d_ws);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + slab_bytes(e, rows));
+  int rc = launch_k2(e, d_panel, rows, ld_panel, ks, accumulate, slab, st);
+  if (rc == SYSID_OK && final) rc = launch_k3(e, ks, slab, part, d_gram, st);
+  return rc;
+}
+int32_t sysid_exp_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
+                     void* stream) {
+  return launch_k1(e, d_in, N, ld, d_panel, ld_panel, static_cast<hipStream_t>(stream), nullptr);
 }
 #endif
 

@@ -66,7 +66,7 @@ __host__ __device__ inline int k1_row_groups(int NJ) {
 // Per-wave LDS region of K1 (doubles, every piece 16-B aligned).  W, Pt, pf (dead once J_c is built)
 // and Z (dead once P is built) share one region.
 struct WLay {
-  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, Z, total;
+  int in, body, W, Pt, Jw, pf, Jc, M, M2, P, H1, tp, Z, total;
 };
 
 __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc) {
@@ -84,10 +84,11 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc)
   l.Pt = take(nv * 3);          // a point on it
   l.pf = take(nc * 3);          // contact points
   l.Z = u0;                     // Z = X J_c
-  const int zend = u0 + ((k * nv + 1) & ~1);
+  l.M2 = u0;                    // second exchange buffer (W, Pt, pf are dead by then; Z comes after)
+  const int zend = u0 + ((((k * nv > k * k) ? k * nv : k * k) + 1) & ~1);
   if (o < zend) o = zend;
   l.Jc = take(k * nv);          // J_c
-  l.M = take(2 * k * k);        // J_c J_c^T, then X = its inverse (two exchange buffers)
+  l.M = take(k * k);            // J_c J_c^T, then X = its inverse (the exchange ends in this buffer)
   l.P = take(nv * nv);          // P = I - J_c^T X J_c
   l.total = o;
   return l;
@@ -512,13 +513,14 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     wsync();
 
-    // ---- M = J_c J_c^T ----
+    // ---- M = J_c J_c^T, into the exchange buffer that makes the k ping-pong steps end in Ms ----
+    double* M0 = (k & 1) ? wr + L.M2 : Ms;
     for (int e = lane; e < k * k; e += 64) {
       const int a = e / k, b = e - a * k;
       double acc = 0.0;
 #pragma unroll 6
       for (int r = 0; r < nv; ++r) acc += Jc[a * nv + r] * Jc[b * nv + r];
-      Ms[e] = acc;
+      M0[e] = acc;
     }
     wsync();
     K1_STAMP(3)
@@ -531,11 +533,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     const double* Xs = Ms;
     {
       double dmax = 0.0;
-      for (int a = 0; a < k; ++a) dmax = fmax(dmax, Ms[a * k + a]);
+      for (int a = 0; a < k; ++a) dmax = fmax(dmax, M0[a * k + a]);
       const double thr = kp.thr_rel * dmax;
       const float rk = k > 0 ? 1.0f / (float)k : 0.0f;
-      double* src = Ms;
-      double* dst = Ms + k * k;
+      double* src = M0;
+      double* dst = (k & 1) ? Ms : wr + L.M2;
       for (int j = 0; j < k; ++j) {
         const double pj = src[j * k + j];
         // three entries per lane per pass: all their loads issue before any store of the pass
@@ -565,7 +567,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         src = dst;
         dst = t;
       }
-      Xs = src;
+      Xs = src;  // == Ms: Z below overwrites the shared region that held the other buffer
     }
     K1_STAMP(4)
 
