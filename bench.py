@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 METRIC = "regressor samples/sec + Gram-build GF/s, 12-DoF, 20k samples, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_MFMA_PEAK_TFS = 78.6  # AMD public spec for MI355X fp64 matrix (not in the container guide)
+MFMA_PEAK_TFS = {"f64": FP64_MFMA_PEAK_TFS, "f32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md (dense)
 
 
 def parse():
@@ -34,6 +35,8 @@ def parse():
     ap.add_argument("--gram-only", action="store_true",
                     help="normal equations only (SURVEY.md §8d config 5): the panel is produced chunk by chunk on "
                          "the device and never returned")
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32", "bf16"],
+                    help="Gram arithmetic for --gram-only (f32/bf16: config 5 throughput, error reported)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="extra all-core C oracle timing (0 = off)")
     return ap.parse_args()
@@ -94,13 +97,15 @@ def main():
     data = generate(model, N, config_index=1 + rank)  # each rank its own shard of the log
     eng = Engine(model, device=local)
     d_in = torch.from_numpy(channel_block(data)).cuda(local)
+    from system_identification_amd.engine import GRAM_PRECISION
     flags = EMIT_ALL
+    tflags = EMIT_ALL | (GRAM_PRECISION[args.precision] if args.gram_only else 0)  # kernels timed below
     stream = torch.cuda.current_stream(local)
     if args.gram_only:
         bufs = eng.alloc_gram_device(N)
 
         def step():
-            eng.build_gram_device(d_in, N, bufs, stream=stream.cuda_stream)
+            eng.build_gram_device(d_in, N, bufs, stream=stream.cuda_stream, precision=args.precision)
             if world > 1:
                 dist.all_reduce(bufs["gram"])
     else:
@@ -135,7 +140,7 @@ def main():
     if args.gram_only:
         n_time = min(N, max(4096, (512 << 20) // (model.nv * eng.panel_ld * 8)))
         tb = eng.alloc_device(n_time, flags)
-        ms = eng.time_stages(d_in, n_time, flags, tb, iters=max(5, args.steps))
+        ms = eng.time_stages(d_in, n_time, tflags, tb, iters=max(5, args.steps))
         del tb
     else:
         ms = eng.time_stages(d_in, N, flags, bufs, iters=max(5, args.steps))
@@ -152,8 +157,9 @@ def main():
                 "avg_launch_ms": round(ms[0], 5)}
     else:
         traffic, src = pmc_traffic("k2_gram_syrk", args.robot, N) if not args.gram_only else (None, None)
+        peak = MFMA_PEAK_TFS[args.precision if args.gram_only else "f64"]
         roof = {"kernel": "k2_gram_syrk", "bound": "mfma", "achieved": round(k2_tfs, 3),
-                "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(k2_tfs / FP64_MFMA_PEAK_TFS, 4),
+                "peak": peak, "unit": "TFLOP/s", "frac": round(k2_tfs / peak, 4),
                 "traffic": traffic, "traffic_source": src, "algorithmic_flops_per_launch": n_time * flops_k2,
                 "avg_launch_ms": round(ms[1], 5)}
 
@@ -162,11 +168,12 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64" if not args.gram_only or args.precision == "f64" else f"f64 panel, {args.precision} Gram",
         "data": "synthetic (SURVEY.md §8d recipe: sinusoidal joints in URDF limits, wobbling base, "
                 "inverse-dynamics torques + noise, trot contacts with LOST=2); no .dat ships with the reference",
         "config": {"workload": f"{args.robot} {N} samples per GPU, " + (
-                       "Gram only (panel chunked on the device)" if args.gram_only else
+                       f"Gram only (panel chunked on the device, {args.precision} Gram)" if args.gram_only else
                        "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
                    "robot": args.robot, "samples_per_gpu": N,
                    "nv": nv, "W": W, "parallelism": f"dp{world}"},

@@ -64,11 +64,16 @@ extern "C" {
 #define SYSID_EMIT_FRICTION 4u  /* stacked B_v and B_c              */
 #define SYSID_EMIT_GRAM     8u  /* G = panelᵀ panel (AᵀA, Aᵀb, bᵀb) */
 #define SYSID_EMIT_ALL     15u
+/* Gram arithmetic (default fp64, the parity path).  Reduced precision for the Gram-only throughput config
+ * (its error is reported, not gated): the panel is rounded to f32 / bf16 as it is
+ * staged into the MFMA tiles, accumulated in f32 per workgroup and in f64 across workgroups. */
+#define SYSID_GRAM_F32     16u
+#define SYSID_GRAM_BF16    32u
 
 typedef struct sysid_engine sysid_engine;
 
 /* ABI version (bumped on any signature or layout change). */
-int32_t sysid_abi_version(void);  /* 3 */
+int32_t sysid_abi_version(void);  /* 4 */
 
 /* Create an engine for one device from a packed model.  Replaces the model construction of
  * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
@@ -113,8 +118,8 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
  * Replaces what Solver.__init__ (src/solver.py:6-29) needs from the stacked arrays: G, g, bᵀb and
  * num_rows = N·nv (the objective scale of :190).  Stream-ordered, no allocation. */
 size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N);
-int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram,
-                                void* d_workspace, size_t workspace_bytes, void* stream);
+int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
+                                double* d_gram, void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Torque-prediction errors: print_tau_prediction_rmse
  * (src/sys_identification.py:421-437) as one reduction over the stacked panel instead of a second

@@ -152,16 +152,26 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
   return SYSID_OK;
 }
 
+// Gram arithmetic selected by the flags: 0 = f64 (parity), 1 = f32 MFMA, 2 = bf16 MFMA (error reported).
+int gram_prec(uint32_t flags) { return (flags & SYSID_GRAM_BF16) ? 2 : (flags & SYSID_GRAM_F32) ? 1 : 0; }
+
 int launch_k2(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
-              double* slab, hipStream_t st) {
+              double* slab, hipStream_t st, int prec) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
   const dim3 g2(e->ngroups * ks), b2(64 * K2_WAVES);
   switch (e->ntc) {
 #define SYSID_K2_CASE(NTC, KC)                                                                               \
   case NTC:                                                                                                 \
-    hipLaunchKernelGGL((k2_gram_syrk<NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles, e->ngroups,  \
-                       ks, e->nslots, accumulate, slab);                                                    \
+    if (prec == 0)                                                                                          \
+      hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles, \
+                         e->ngroups, ks, e->nslots, accumulate, slab);                                      \
+    else if (prec == 1)                                                                                     \
+      hipLaunchKernelGGL((k2_gram_syrk<float, NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles,  \
+                         e->ngroups, ks, e->nslots, accumulate, slab);                                      \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, 32>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles,    \
+                         e->ngroups, ks, e->nslots, accumulate, slab);                                      \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
     SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
@@ -205,7 +215,7 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
       return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, sb + pb);
     double* slab = static_cast<double*>(d_ws);
     double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + sb);
-    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st)) != SYSID_OK) return rc;
+    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
     if ((rc = launch_k3(e, ks, slab, part, d_gram, st)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
@@ -229,8 +239,8 @@ size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {
   return align256((size_t)rows * e->ldp * sizeof(double)) + slab_bytes(e, rows) + part_bytes(e, rows);
 }
 
-int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram, void* d_ws,
-                        size_t ws_bytes, hipStream_t st) {
+int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
+                        void* d_ws, size_t ws_bytes, hipStream_t st) {
   if (N <= 0) return SYSID_OK;
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes(e, N))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, gram_ws_bytes(e, N));
@@ -244,7 +254,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     const int64_t n = std::min(C, N - c0);
     if ((rc = launch_k1(e, d_in + c0, n, ld, panel, e->ldp, st, nullptr)) != SYSID_OK) return rc;
     const int ks = std::min(ks0, ksplit_for(e, n * e->nv));
-    if ((rc = launch_k2(e, panel, n * e->nv, e->ldp, ks, c0 > 0, slab, st)) != SYSID_OK) return rc;
+    if ((rc = launch_k2(e, panel, n * e->nv, e->ldp, ks, c0 > 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
   }
   return launch_k3(e, ks0, slab, part, d_gram, st);
 }
@@ -272,7 +282,7 @@ int launch_k4(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t 
 
 extern "C" {
 
-int32_t sysid_abi_version(void) { return 3; }
+int32_t sysid_abi_version(void) { return 4; }
 
 const char* sysid_last_error(const sysid_engine* e) { return e ? e->err.c_str() : g_thread_error.c_str(); }
 
@@ -541,8 +551,8 @@ size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N) {
   return gram_ws_bytes(e, N);
 }
 
-int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_gram,
-                                void* d_ws, size_t ws_bytes, void* stream) {
+int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
+                                double* d_gram, void* d_ws, size_t ws_bytes, void* stream) {
   if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
   if (N < 0 || ld < N || (N > 0 && !d_in) || !d_gram)
     return set_err(e, SYSID_E_INVALID, "bad arguments (N=%lld ld=%lld)", (long long)N, (long long)ld);
@@ -552,7 +562,7 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
     HIP_TRY(e, hipMemsetAsync(d_gram, 0, (size_t)e->ncol * e->ncol * sizeof(double), st));
     return SYSID_OK;
   }
-  return launch_gram_chunked(e, d_in, N, ld, d_gram, d_ws, ws_bytes, st);
+  return launch_gram_chunked(e, d_in, N, ld, flags, d_gram, d_ws, ws_bytes, st);
 }
 
 size_t sysid_tau_error_workspace_bytes(const sysid_engine* e, int64_t N) {
@@ -687,7 +697,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
                                   hipMemcpyHostToDevice, st));
     r0 += nrows[k];
   }
-  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, e->d_gram, e->d_ws, e->ws_cap, st)
+  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
   if (rc != SYSID_OK) return rc;
   const size_t pitch = (size_t)e->ldp * sizeof(double);
@@ -802,7 +812,7 @@ int32_t sysid_exp_k2(sysid_engine* e, const double* d_panel, int64_t N, int64_t 
   const int ks = ksplit_for(e, rows);
   double* slab = static_cast<double*>(d_ws);
   double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + slab_bytes(e, rows));
-  int rc = launch_k2(e, d_panel, rows, ld_panel, ks, accumulate, slab, st);
+  int rc = launch_k2(e, d_panel, rows, ld_panel, ks, accumulate, slab, st, 0);
   if (rc == SYSID_OK && final) rc = launch_k3(e, ks, slab, part, d_gram, st);
   return rc;
 }

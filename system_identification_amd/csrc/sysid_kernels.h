@@ -725,18 +725,28 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 // both the A layout (A[i=l&15][k=l>>4]) and the B layout (B[k=l>>4][j=l&15]) of v_mfma_f64_16x16x4_f64.
 // ------------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef float flt4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int K2_SPW = 2;   // super-tiles per wave
+
+// Reduced-precision Gram (error reported, not gated): T = float runs the same
+// kernel on v_mfma_f32_16x16x4_f32 (panel rounded to f32 while staged, f32 accumulation per workgroup,
+// f64 across workgroups in K3); bf16 is k2_gram_syrk_bf16 below.
+template <typename T> struct K2Acc;
+template <> struct K2Acc<double> { typedef dbl4 type; };
+template <> struct K2Acc<float> { typedef flt4 type; };
 
 __host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) / 32) * 32 + 16; }
 
-template <int NTC, int KC>
+template <typename T, int NTC, int KC>
 __global__ void __launch_bounds__(64 * K2_WAVES)
 k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
              int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+  typedef typename K2Acc<T>::type accT;
   constexpr int STRIDE = k2_stride(NTC);
-  constexpr int BUF = KC * STRIDE;                       // doubles per LDS buffer
+  constexpr int BUF = KC * STRIDE;                       // elements per LDS buffer
   constexpr int NT = 64 * K2_WAVES;
-  __shared__ double lds[2 * BUF];
+  __shared__ T lds[2 * BUF];
   const int group = blockIdx.x % ngroups;
   const int ks = blockIdx.x / ngroups;
   const int64_t q4 = rows / 4;
@@ -771,10 +781,14 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
       st[u] = (used[u] && x < lim) ? src[x] : double2{0.0, 0.0};
     }
   };
-  auto store_chunk = [&](double* b) {
+  auto store_chunk = [&](T* b) {
 #pragma unroll
-    for (int u = 0; u < PER; ++u)
-      if (used[u]) *reinterpret_cast<double2*>(b + loff[u]) = st[u];
+    for (int u = 0; u < PER; ++u) {
+      if (used[u]) {
+        if constexpr (sizeof(T) == 8) *reinterpret_cast<double2*>(b + loff[u]) = st[u];
+        else *reinterpret_cast<float2*>(b + loff[u]) = make_float2((float)st[u].x, (float)st[u].y);
+      }
+    }
   };
 
   // fragment columns of this wave: f = 4*s + {I0, I0+1, J0, J0+1} (16-column blocks)
@@ -797,11 +811,11 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
       foff[4 * s + u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
     }
   }
-  dbl4 acc[K2_SPW][4];
+  accT acc[K2_SPW][4];
 #pragma unroll
   for (int s = 0; s < K2_SPW; ++s)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[s][t] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
 
   const int64_t nchunks = (r1 - r0 + KC - 1) / KC;
   __syncthreads();  // LDS zeroed
@@ -811,25 +825,30 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
   }
   __syncthreads();
   for (int64_t c = 0; c < nchunks; ++c) {
-    const double* cur = lds + (c & 1) * BUF;
+    const T* cur = lds + (c & 1) * BUF;
     if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * KC);
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
-      double x[4 * K2_SPW];
+      T x[4 * K2_SPW];
 #pragma unroll
       for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = cur[foff[u] + kk * STRIDE];
 #pragma unroll
       for (int s = 0; s < K2_SPW; ++s) {
-        if (need[s][0]) acc[s][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 2], acc[s][0], 0, 0, 0);
-        if (need[s][1]) acc[s][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 0], x[4 * s + 3], acc[s][1], 0, 0, 0);
-        if (need[s][2]) acc[s][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 2], acc[s][2], 0, 0, 0);
-        if (need[s][3]) acc[s][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + 1], x[4 * s + 3], acc[s][3], 0, 0, 0);
+        constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (!need[s][t]) continue;
+          if constexpr (sizeof(T) == 8)
+            acc[s][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
+          else
+            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
+        }
       }
     }
     if (c + 1 < nchunks) store_chunk(lds + ((c + 1) & 1) * BUF);
     __syncthreads();
   }
-  // D layout of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
+  // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
 #pragma unroll
   for (int s = 0; s < K2_SPW; ++s) {
     if (!live[s]) continue;
@@ -838,8 +857,145 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
       double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        double* x = o + ((lane >> 4) + 4 * j) * 16 + (lane & 15);
-        *x = accumulate ? *x + acc[s][t][j] : acc[s][t][j];  // chunked Gram: slabs carry over chunks
+        const int row = sizeof(T) == 8 ? (lane >> 4) + 4 * j : 4 * (lane >> 4) + j;
+        double* x = o + row * 16 + (lane & 15);
+        const double v = (double)acc[s][t][j];
+        *x = accumulate ? *x + v : v;  // chunked Gram: slabs carry over chunks
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2 bf16: the same super-tile decomposition on v_mfma_f32_16x16x32_bf16.  A chunk of KC (a multiple of
+// 32) rows is staged column-major in LDS (column stride CS = KC + 8 bf16), so the fragment of lane l —
+// 8 consecutive rows 8(l>>4).. of column (l & 15) of a 16-column block, which is both the A layout
+// A[i = l&15][k = 8(l>>4) + j] and the B layout B[k][j = l&15] — is one 16-byte ds_read.  Staging item
+// = (column pair, 8-row group): eight 16-byte global loads, rounded f64 -> bf16 (RNE via f32), two
+// 16-byte LDS stores.  f32 accumulation per workgroup, f64 across workgroups (K3).
+// ------------------------------------------------------------------------------------------------
+template <int NTC, int KC>
+__global__ void __launch_bounds__(64 * K2_WAVES)
+k2_gram_syrk_bf16(const double* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+                  int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+  static_assert(KC % 32 == 0, "bf16 K2 chunks are whole 32-row k-steps");
+  constexpr int NCOL = NTC * 16;
+  constexpr int CS = KC + 8;
+  constexpr int BUF = NCOL * CS;
+  constexpr int NT = 64 * K2_WAVES;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
+  const int group = blockIdx.x % ngroups;
+  const int ks = blockIdx.x / ngroups;
+  const int64_t q4 = rows / 4;
+  const int64_t r0 = 4 * (q4 * ks / ksplit);
+  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sbase = (group * K2_WAVES + wave) * K2_SPW;
+
+  // zero both buffers once: columns >= ldp are never staged and must read as 0
+  for (int x = threadIdx.x; x < 2 * BUF; x += NT) lds[x] = (__bf16)0.0f;
+
+  const int npair = (int)(ldp >> 1);
+  constexpr int PER = (NTC * 8 * (KC / 8) + NT - 1) / NT;
+  int cp[PER], ro[PER];
+  bool used[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int it = threadIdx.x + u * NT;
+    used[u] = it < npair * (KC / 8);
+    ro[u] = used[u] ? it / npair : 0;
+    cp[u] = used[u] ? it - ro[u] * npair : 0;
+  }
+  double2 st[PER][8];
+  auto load_chunk = [&](int64_t c0) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int64_t r = c0 + 8 * ro[u] + t;
+        st[u][t] = (used[u] && r < r1) ? reinterpret_cast<const double2*>(panel + r * ldp)[cp[u]]
+                                       : double2{0.0, 0.0};
+      }
+  };
+  auto store_chunk = [&](__bf16* b) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      if (!used[u]) continue;
+      bf16x8 lo, hi;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        lo[t] = (__bf16)(float)st[u][t].x;
+        hi[t] = (__bf16)(float)st[u][t].y;
+      }
+      *reinterpret_cast<bf16x8*>(b + (2 * cp[u]) * CS + 8 * ro[u]) = lo;
+      *reinterpret_cast<bf16x8*>(b + (2 * cp[u] + 1) * CS + 8 * ro[u]) = hi;
+    }
+  };
+
+  int foff[4 * K2_SPW];
+  bool live[K2_SPW];
+  bool need[K2_SPW][4];
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s) {
+    const int2 sp = supers[sbase + s];
+    live[s] = sp.x >= 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int I = 2 * sp.x + (t >> 1), J = 2 * sp.y + (t & 1);
+      need[s][t] = live[s] && I <= J && J < NTC;
+    }
+    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
+      foff[4 * s + u] = (16 * b + (lane & 15)) * CS + 8 * (lane >> 4);
+    }
+  }
+  flt4 acc[K2_SPW][4];
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[s][t] = flt4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nchunks = (r1 - r0 + KC - 1) / KC;
+  __syncthreads();  // LDS zeroed
+  if (nchunks > 0) {
+    load_chunk(r0);
+    store_chunk(lds);
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < nchunks; ++c) {
+    const __bf16* cur = lds + (c & 1) * BUF;
+    if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * KC);
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 32) {
+      bf16x8 x[4 * K2_SPW];
+#pragma unroll
+      for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = *reinterpret_cast<const bf16x8*>(cur + foff[u] + kk);
+#pragma unroll
+      for (int s = 0; s < K2_SPW; ++s) {
+        constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (need[s][t])
+            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t],
+                                                               0, 0, 0);
+      }
+    }
+    if (c + 1 < nchunks) store_chunk(lds + ((c + 1) & 1) * BUF);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s) {
+    if (!live[s]) continue;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double* x = o + (4 * (lane >> 4) + j) * 16 + (lane & 15);
+        const double v = (double)acc[s][t][j];
+        *x = accumulate ? *x + v : v;
       }
     }
   }

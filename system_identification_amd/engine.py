@@ -25,6 +25,8 @@ EMIT_TAU = 2
 EMIT_FRICTION = 4
 EMIT_GRAM = 8
 EMIT_ALL = 15
+GRAM_F32, GRAM_BF16 = 16, 32
+GRAM_PRECISION = {"f64": 0, "f32": GRAM_F32, "bf16": GRAM_BF16}
 
 LIB_NAME = "libsysid.so"
 LIB_PATH = os.environ.get("SYSID_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
@@ -64,7 +66,8 @@ SIGNATURES = [
     ("sysid_tau_error", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _dp, _dp]),
     ("sysid_tau_error_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
     ("sysid_tau_error_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _vp, _c.c_size_t, _vp]),
-    ("sysid_build_gram_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _c.c_size_t, _vp]),
+    ("sysid_build_gram_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _vp, _c.c_size_t,
+                                             _vp]),
 ]
 
 _LIB = None
@@ -258,14 +261,15 @@ class Engine:
             "ws": torch.empty(max(self.gram_workspace_bytes(N), 256), dtype=torch.uint8, device=dev),
         }
 
-    def build_gram_device(self, d_in, N: int, bufs: dict, stream=None):
-        """Normal equations of N samples without materialising the N·nv-row panel (stream-ordered)."""
+    def build_gram_device(self, d_in, N: int, bufs: dict, stream=None, precision: str = "f64"):
+        """Normal equations of N samples without materialising the N·nv-row panel (stream-ordered).
+        precision: "f64" (parity), "f32" or "bf16" (MFMA in reduced precision, error reported)."""
         import torch
         if d_in.dtype != torch.float64 or not d_in.is_cuda or d_in.shape[0] != self.in_rows:
             raise ValueError(f"d_in must be a float64 CUDA tensor with {self.in_rows} channel rows")
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.sysid_build_gram_device(
-            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)),
+            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)), GRAM_PRECISION[precision],
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)

@@ -226,6 +226,30 @@ def test_tau_prediction_rmse_reduction(robot, N):
         e.tau_error(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], phi[:-1])
 
 
+@pytest.mark.parametrize("robot,N", [("spot", 20000), ("g1_29dof", 5000)])
+def test_reduced_precision_gram(robot, N):
+    """f32 / bf16 MFMA Grams (error reported, not gated) against the f64 Gram of the
+    same panel; normwise relative error printed, bounded loosely (f32 ~1e-7, bf16 ~1e-3 expected)."""
+    import torch
+    model = load_robot(robot)
+    e = eng(robot)
+    d = generate(model, N, config_index=7)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    out = {}
+    for prec in ("f64", "f32", "bf16"):
+        bufs = e.alloc_gram_device(N)
+        e.build_gram_device(din, N, bufs, precision=prec)
+        torch.cuda.synchronize()
+        out[prec] = bufs["gram"].cpu().numpy()
+    G = out["f64"]
+    nrm = np.linalg.norm(G)
+    errs = {p: np.linalg.norm(out[p] - G) / nrm for p in ("f32", "bf16")}
+    print(f"{robot} N={N} Gram normwise rel. error: f32 {errs['f32']:.2e}  bf16 {errs['bf16']:.2e}")
+    assert errs["f32"] < 1e-5
+    assert errs["bf16"] < 3e-2
+    assert np.array_equal(out["f32"], out["f32"].T) and np.array_equal(out["bf16"], out["bf16"].T)
+
+
 def test_rccl_gram_allreduce_single_rank():
     """sysid_allreduce_gram over a one-rank RCCL communicator is the identity on the Gram (the N > 1 path
     needs more GPUs than a test box has; its host logic is covered by the gloo tests)."""
