@@ -99,6 +99,15 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
                     double* Y_proj, double* tau_proj, double* B_v, double* B_c,
                     double* gram, double* Atb, double* btb);
 
+/* get_full_regressor_force (src/sys_identification.py:391-399), batched: the unprojected joint-torque
+ * regressor Y (N·nv x 10·nb) and F = Sᵀ tau + J_cᵀ lambda (N·nv), lambda = the measured forces
+ * ee_force (3·n_contact x ld, channel-major, foot k in rows 3k..3k+2) of the feet in contact, in foot
+ * order (:137-146).  A sample whose int(sum(cnt)) differs from its number of non-zero feet is rejected with
+ * SYSID_E_CONTACT (the reference's J_cᵀ @ lambda has mismatched shapes there).  Y or F may be NULL. */
+int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, const double* ddq,
+                         const double* tau, const double* ee_force, const double* cnt, int64_t N, int64_t ld,
+                         double* Y, double* F);
+
 /* Device workspace needed by sysid_build_device for N samples (bytes, 256-B aligned pieces). */
 size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags);
 

@@ -231,6 +231,29 @@ def get_proj_friction_regressors(model, q, dq, ddq, cnt):
     return P @ S.T @ np.diag(dq[bd:]), P @ S.T @ np.diag(np.sign(dq[bd:]))
 
 
+def compute_lambda(model, force, cnt):
+    """src/sys_identification.py:137-146 (m = int(sum(cnt)) entries, one 3-block per truthy foot)."""
+    m = int(np.sum(cnt))
+    lam = np.zeros(3 * m)
+    j = 0
+    for i in range(len(model.contact_frames())):
+        if cnt[i]:
+            lam[j:j + 3] = force[3 * i:3 * (i + 1)]
+            j += 3
+    return lam
+
+
+def get_full_regressor_force(model, q, dq, ddq, tau, ee_force, cnt):
+    """src/sys_identification.py:391-399: Y (unprojected) and F = S^T tau + J_c^T lambda."""
+    q, dq, ddq = (np.asarray(x, dtype=np.float64) for x in (q, dq, ddq))
+    d = forward_pass(model, q, dq, ddq)
+    Y = joint_torque_regressor(model, q, dq, ddq, data=d)
+    J_c = compute_J_c(model, d, cnt)
+    lam = compute_lambda(model, np.asarray(ee_force, dtype=np.float64), cnt)
+    F = selection_matrix(model).T @ np.asarray(tau, dtype=np.float64) + J_c.T @ lam
+    return Y, F
+
+
 def get_projected_y_tau(model, q, dq, ddq, torque, cnt):
     """demo/spot_identification.py:37-45 + :84-85 (per-sample loop, vstack/hstack)."""
     Y, T = [], []

@@ -38,7 +38,7 @@ struct sysid_engine {
   int device = 0;
   int cus = 256;
   hipStream_t stream = nullptr;
-  int nq = 0, nv = 0, nj = 0, nb = 0, nc = 0, wy = 0, w = 0, ncol = 0, ldp = 0, in_rows = 0;
+  int nq = 0, nv = 0, nj = 0, nb = 0, nc = 0, wy = 0, w = 0, ncol = 0, ldp = 0, in_rows = 0, in_lds = 0;
   // K1
   K1Params kp{};
   uint32_t* d_mimg = nullptr;
@@ -128,8 +128,12 @@ const void* k1_fn(int variant) {
 }
 
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
-              hipStream_t st, double* dbg) {
+              hipStream_t st, double* dbg, int full = 0) {
   K1Params kp = e->kp;
+  if (full) {
+    kp.full = 1;
+    kp.in_rows = e->in_lds;
+  }
   kp.out_cols = (int)std::min<int64_t>(ld_panel, e->ldp);
   const int64_t waves_needed = N;
   const int64_t cap = (int64_t)e->cus * e->k1_blocks_per_cu;
@@ -362,7 +366,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     csupp[c] = mask;
   }
   const int in_rows = nq + 2 * nv + nja + nc;
-  if (in_rows > IN_MAX) return set_err(nullptr, SYSID_E_MODEL, "too many input channels (%d > %d)", in_rows, IN_MAX);
+  const int in_lds = in_rows + 3 * nc;  // + measured foot forces in the full-force mode
+  if (in_lds > IN_MAX) return set_err(nullptr, SYSID_E_MODEL, "too many input channels (%d > %d)", in_lds, IN_MAX);
 
   // model image (layout sysid_dev::mimg_layout)
   const int maxch_tpl = maxch <= 4 ? 4 : 16;
@@ -396,10 +401,12 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->ncol = e->w + 1;
   e->ldp = (e->ncol + 1) & ~1;
   e->in_rows = in_rows;
-  const WLay WL = wave_layout(in_rows, nv, NJ, nc);
+  e->in_lds = in_lds;
+  const WLay WL = wave_layout(in_lds, nv, NJ, nc);
   K1Params& kp = e->kp;
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
+  kp.in_lds = in_lds; kp.full = 0;
   kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL.total; kp.out_cols = e->ldp;
   kp.rg = k1_row_groups(NJ);
   kp.thr_rel = 1e-13;
@@ -629,6 +636,56 @@ int32_t sysid_tau_error(sysid_engine* e, const double* q, const double* dq, cons
   return SYSID_OK;
 }
 
+int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
+                         const double* ee_force, const double* cnt, int64_t N, int64_t ld, double* Y, double* F) {
+  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
+  if (N < 0 || ld < N) return set_err(e, SYSID_E_INVALID, "bad N/ld (%lld/%lld)", (long long)N, (long long)ld);
+  if (N > 0 && (!q || !dq || !ddq || (!tau && e->nj) || (!cnt && e->nc) || (!ee_force && e->nc)))
+    return set_err(e, SYSID_E_INVALID, "null input buffer");
+  if (N == 0) return SYSID_OK;
+  // reference: lambda has 3*int(sum(cnt)) entries and J_c one 3-row block per truthy foot; J_c^T lambda
+  // is only defined when the two agree (otherwise numpy raises a shape error there)
+  for (int64_t s = 0; s < N && e->nc; ++s) {
+    double sum = 0.0;
+    int64_t nz = 0;
+    for (int c = 0; c < e->nc; ++c) {
+      const double v = cnt[(int64_t)c * ld + s];
+      sum += v;
+      nz += v != 0.0;
+    }
+    if (std::trunc(sum) != (double)nz)
+      return set_err(e, SYSID_E_CONTACT, "sample %lld: int(sum(contact)) = %g != %lld feet in contact (J_c^T lambda "
+                     "has mismatched shapes in the reference)", (long long)s, std::trunc(sum), (long long)nz);
+  }
+  HIP_TRY(e, hipSetDevice(e->device));
+  const int64_t rows = N * e->nv;
+  int rc;
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_lds * N * sizeof(double)))) return rc;
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
+    return rc;
+  hipStream_t st = e->stream;
+  const size_t rowb = (size_t)N * sizeof(double);
+  const double* srcs[6] = {q, dq, ddq, tau, cnt, ee_force};
+  const int nrows[6] = {e->nq, e->nv, e->nv, e->nj, e->nc, 3 * e->nc};
+  int64_t r0 = 0;
+  for (int k = 0; k < 6; ++k) {
+    if (nrows[k] > 0)
+      HIP_TRY(e, hipMemcpy2DAsync(e->d_in + r0 * N, rowb, srcs[k], (size_t)ld * sizeof(double), rowb, nrows[k],
+                                  hipMemcpyHostToDevice, st));
+    r0 += nrows[k];
+  }
+  if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, st, nullptr, 1)) != SYSID_OK) return rc;
+  const size_t pitch = (size_t)e->ldp * sizeof(double);
+  if (Y)
+    HIP_TRY(e, hipMemcpy2DAsync(Y, (size_t)e->wy * sizeof(double), e->d_panel, pitch, (size_t)e->wy * sizeof(double),
+                                rows, hipMemcpyDeviceToHost, st));
+  if (F)
+    HIP_TRY(e, hipMemcpy2DAsync(F, sizeof(double), e->d_panel + e->w, pitch, sizeof(double), rows,
+                                hipMemcpyDeviceToHost, st));
+  HIP_TRY(e, hipStreamSynchronize(st));
+  return SYSID_OK;
+}
+
 int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                           int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, int32_t iters, double* ms) {
   if (!e || !ms || iters <= 0) return set_err(e, SYSID_E_INVALID, "bad arguments");
@@ -753,7 +810,7 @@ int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6) {
 
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
   if (!e || !offsets12) return SYSID_E_INVALID;
-  const WLay L = wave_layout(e->in_rows, e->nv, e->nb + 1, e->nc);
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc);
   const int o[12] = {L.in, L.body, L.W, L.Pt, L.Jw, L.pf, L.Jc, L.M, L.P, L.H1, L.tp, L.total};
   for (int k = 0; k < 12; ++k) offsets12[k] = o[k];
   return SYSID_OK;
@@ -762,7 +819,7 @@ int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
 int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
                         const double* cnt, double* lds_image, int64_t image_doubles) {
   if (!e || !lds_image) return set_err(e, SYSID_E_INVALID, "null argument");
-  const WLay L = wave_layout(e->in_rows, e->nv, e->nb + 1, e->nc);
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc);
   if (image_doubles < L.total) return set_err(e, SYSID_E_INVALID, "image needs %d doubles", L.total);
   HIP_TRY(e, hipSetDevice(e->device));
   int rc = sysid_build(e, q, dq, ddq, tau, cnt, 1, 1, SYSID_EMIT_Y, nullptr, nullptr, nullptr, nullptr, nullptr,

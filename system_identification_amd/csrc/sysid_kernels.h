@@ -97,6 +97,8 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc)
 struct K1Params {
   int nq, nv, NJ, nc, bd, nj, maxdepth, wy, w, ncol, in_rows, maxch, has_ff, ff0, mimg_dbl, wave_dbl;
   int out_cols;     // columns written per panel row (ncol rounded up to the panel's even stride)
+  int in_lds;       // input channels the LDS layout holds (in_rows of the full-force mode)
+  int full;         // 1: get_full_regressor_force mode (P = I, tau column = S^T tau + J_c^T lambda)
   int rg;           // row groups of the regressor-column phase (lanes = bodies x rg)
   double thr_rel;   // pivot cut of the J_c J_c^T inversion (relative to its max diagonal)
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
@@ -182,6 +184,9 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 }
+
+// Panel stores (plain: non-temporal stores measured equal on Spot and 2.5x slower K1 on G1).
+__device__ __forceinline__ void panel_store(double2* p, double2 v) { *p = v; }
 
 #ifdef SYSID_STAMPS
 // Diagnostics build: per-phase shader-clock deltas accumulated in registers (s_memtime is uniform, so
@@ -303,7 +308,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const int nv = NVC > 0 ? NVC : kp.nv;
   const int nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const WLay L = wave_layout(IN, nv, NJ, nc);
+  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc);
   double* wr = smem + kp.mimg_dbl + wave * kp.wave_dbl;
   double* body = wr + L.body;
   double* Ws = wr + L.W;
@@ -513,82 +518,91 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     wsync();
 
-    // ---- M = J_c J_c^T, into the exchange buffer that makes the k ping-pong steps end in Ms ----
-    double* M0 = (k & 1) ? wr + L.M2 : Ms;
-    for (int e = lane; e < k * k; e += 64) {
-      const int a = e / k, b = e - a * k;
-      double acc = 0.0;
-#pragma unroll 6
-      for (int r = 0; r < nv; ++r) acc += Jc[a * nv + r] * Jc[b * nv + r];
-      M0[e] = acc;
-    }
-    wsync();
-    K1_STAMP(3)
-
-    // ---- X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, ping-ponging between two LDS buffers ----
-    // One pivot per step (no square roots, one reciprocal); every entry of a step reads only the
-    // previous buffer, so each step is a single wave-synchronous pass.  A pivot <= thr_rel * max diag
-    // (a contact row dependent on the kept ones) is dropped: ip = 0 zeroes its row and column and
-    // leaves the rest untouched, i.e. X is the inverse on the kept rows, as pinv treats them.
-    const double* Xs = Ms;
-    {
-      double dmax = 0.0;
-      for (int a = 0; a < k; ++a) dmax = fmax(dmax, M0[a * k + a]);
-      const double thr = kp.thr_rel * dmax;
-      const float rk = k > 0 ? 1.0f / (float)k : 0.0f;
-      double* src = M0;
-      double* dst = (k & 1) ? Ms : wr + L.M2;
-      for (int j = 0; j < k; ++j) {
-        const double pj = src[j * k + j];
-        // three entries per lane per pass: all their loads issue before any store of the pass
-        for (int e0 = lane; e0 < k * k; e0 += 192) {
-          int r[3], c[3];
-          double arc[3], arj[3], ajc[3];
-#pragma unroll
-          for (int u = 0; u < 3; ++u) {
-            const int e = e0 + 64 * u;
-            const int ee = e < k * k ? e : 0;
-            r[u] = (int)(((float)ee + 0.5f) * rk);  // exact: ee < 24*24
-            c[u] = ee - r[u] * k;
-            arc[u] = src[ee];
-            arj[u] = src[r[u] * k + j];
-            ajc[u] = src[j * k + c[u]];
-          }
-          const double ip = pj > thr ? 1.0 / pj : 0.0;
-#pragma unroll
-          for (int u = 0; u < 3; ++u) {
-            const double v = r[u] == j ? (c[u] == j ? ip : ajc[u] * ip)
-                                       : (c[u] == j ? -arj[u] * ip : arc[u] - arj[u] * ajc[u] * ip);
-            if (e0 + 64 * u < k * k) dst[e0 + 64 * u] = v;
-          }
-        }
-        wsync();
-        double* t = src;
-        src = dst;
-        dst = t;
+    if (kp.full) {
+      // get_full_regressor_force (src/sys_identification.py:391-399): no projection
+      for (int e = lane; e < nv * nv; e += 64) {
+        const int a = e / nv;
+        Ps[e] = e - a * nv == a ? 1.0 : 0.0;
       }
-      Xs = src;  // == Ms: Z below overwrites the shared region that held the other buffer
-    }
-    K1_STAMP(4)
+      wsync();
+    } else {
+      // ---- M = J_c J_c^T, into the exchange buffer that makes the k ping-pong steps end in Ms ----
+      double* M0 = (k & 1) ? wr + L.M2 : Ms;
+      for (int e = lane; e < k * k; e += 64) {
+        const int a = e / k, b = e - a * k;
+        double acc = 0.0;
+#pragma unroll 6
+        for (int r = 0; r < nv; ++r) acc += Jc[a * nv + r] * Jc[b * nv + r];
+        M0[e] = acc;
+      }
+      wsync();
+      K1_STAMP(3)
 
-    // ---- Z = X J_c ;  P = I - J_c^T Z ----
-    double* Zs = wr + L.Z;
-    for (int e = lane; e < k * nv; e += 64) {
-      const int a = e / nv, r = e - a * nv;
-      double acc = 0.0;
+      // ---- X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, ping-ponging between two LDS buffers ----
+      // One pivot per step (no square roots, one reciprocal); every entry of a step reads only the
+      // previous buffer, so each step is a single wave-synchronous pass.  A pivot <= thr_rel * max diag
+      // (a contact row dependent on the kept ones) is dropped: ip = 0 zeroes its row and column and
+      // leaves the rest untouched, i.e. X is the inverse on the kept rows, as pinv treats them.
+      const double* Xs = Ms;
+      {
+        double dmax = 0.0;
+        for (int a = 0; a < k; ++a) dmax = fmax(dmax, M0[a * k + a]);
+        const double thr = kp.thr_rel * dmax;
+        const float rk = k > 0 ? 1.0f / (float)k : 0.0f;
+        double* src = M0;
+        double* dst = (k & 1) ? Ms : wr + L.M2;
+        for (int j = 0; j < k; ++j) {
+          const double pj = src[j * k + j];
+          // three entries per lane per pass: all their loads issue before any store of the pass
+          for (int e0 = lane; e0 < k * k; e0 += 192) {
+            int r[3], c[3];
+            double arc[3], arj[3], ajc[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+              const int e = e0 + 64 * u;
+              const int ee = e < k * k ? e : 0;
+              r[u] = (int)(((float)ee + 0.5f) * rk);  // exact: ee < 24*24
+              c[u] = ee - r[u] * k;
+              arc[u] = src[ee];
+              arj[u] = src[r[u] * k + j];
+              ajc[u] = src[j * k + c[u]];
+            }
+            const double ip = pj > thr ? 1.0 / pj : 0.0;
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+              const double v = r[u] == j ? (c[u] == j ? ip : ajc[u] * ip)
+                                         : (c[u] == j ? -arj[u] * ip : arc[u] - arj[u] * ajc[u] * ip);
+              if (e0 + 64 * u < k * k) dst[e0 + 64 * u] = v;
+            }
+          }
+          wsync();
+          double* t = src;
+          src = dst;
+          dst = t;
+        }
+        Xs = src;  // == Ms: Z below overwrites the shared region that held the other buffer
+      }
+      K1_STAMP(4)
+
+      // ---- Z = X J_c ;  P = I - J_c^T Z ----
+      double* Zs = wr + L.Z;
+      for (int e = lane; e < k * nv; e += 64) {
+        const int a = e / nv, r = e - a * nv;
+        double acc = 0.0;
 #pragma unroll 4
-      for (int b = 0; b < k; ++b) acc += Xs[a * k + b] * Jc[b * nv + r];
-      Zs[e] = acc;
-    }
-    wsync();
-    for (int e = lane; e < nv * nv; e += 64) {
-      const int a = e / nv, b = e - a * nv;
-      double acc = 0.0;
+        for (int b = 0; b < k; ++b) acc += Xs[a * k + b] * Jc[b * nv + r];
+        Zs[e] = acc;
+      }
+      wsync();
+      for (int e = lane; e < nv * nv; e += 64) {
+        const int a = e / nv, b = e - a * nv;
+        double acc = 0.0;
 #pragma unroll 4
-      for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Zs[j * nv + b];
-      Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+        for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Zs[j * nv + b];
+        Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+      }
+      wsync();
     }
-    wsync();
     K1_STAMP(5)
 
     // ---- H1 = P[:, ff] J_w[:, ff]^T ;  tp = P S^T tau ----
@@ -604,6 +618,25 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         double acc = 0.0;
 #pragma unroll 4
         for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
+        if (kp.full) {
+          // + J_c^T lambda, lambda = the measured forces of the feet in contact in foot order, world axes
+          // (LOCAL_WORLD_ALIGNED).  J_c here is in base axes, J_c,world = R_b J_c, so lambda is moved to
+          // base axes with R_b^T (R_b = the base quaternion's matrix, unnormalised like pinocchio's).
+          double Rb[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+          if (kp.has_ff && jtype[1] == JT_FREEFLYER) {
+            const int iq = idx_q[1];
+            quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], Rb);
+          }
+          const double* lam = cnt + nc;
+          for (int rho = 0, c = -1; rho < k; ++rho) {
+            const int comp = rho % 3;
+            if (comp == 0)
+              for (++c; c < nc && cnt[c] == 0.0; ++c) {}
+            const double* lw = lam + 3 * c;
+            const double lb = Rb[comp] * lw[0] + Rb[3 + comp] * lw[1] + Rb[6 + comp] * lw[2];
+            acc += Jc[rho * nv + r] * lb;
+          }
+        }
         tps[r] = acc;
       }
     }
@@ -669,7 +702,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
         double2* o2 = reinterpret_cast<double2*>(oi + (int64_t)r * ldp);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) o2[c] = make_double2(y[2 * c], y[2 * c + 1]);
+        for (int c = 0; c < 5; ++c) panel_store(o2 + c, make_double2(y[2 * c], y[2 * c + 1]));
       }
     }
 
@@ -691,7 +724,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const double fr = pr[jc] * sc;
           v2[u] = jj < 2 * nja ? fr : (kp.wy + jj == kp.w ? tps[r] : 0.0);  // pad: keep lines whole
         }
-        *reinterpret_cast<double2*>(out + (int64_t)r * ldp + kp.wy + 2 * m) = make_double2(v2[0], v2[1]);
+        panel_store(reinterpret_cast<double2*>(out + (int64_t)r * ldp + kp.wy + 2 * m), make_double2(v2[0], v2[1]));
       }
     }
     K1_STAMP(7)

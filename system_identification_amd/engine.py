@@ -55,6 +55,7 @@ SIGNATURES = [
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
+    ("sysid_build_full", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _dp, _dp]),
     ("sysid_dat_shape", _c.c_int32, [_c.c_char_p, _c.POINTER(_c.c_int64), _c.POINTER(_c.c_int64)]),
     ("sysid_dat_read", _c.c_int32, [_c.c_char_p, _c.POINTER(_c.c_float), _c.c_int64, _c.c_int64, _c.c_int32]),
     ("sysid_io_last_error", _c.c_char_p, []),
@@ -189,6 +190,26 @@ class Engine:
         if G is not None:
             out["gram"], out["Atb"], out["btb"], out["num_rows"] = G, g, float(btb[0]), R
         return out
+
+    def build_full(self, q, dq, ddq, tau, ee_force, cnt):
+        """Unprojected regressor Y (N·nv x 10 nb) and F = Sᵀ tau + J_cᵀ lambda (N·nv,), K1 in full-force mode."""
+        ins = []
+        for a, rows, name in ((q, self.nq, "q"), (dq, self.nv, "dq"), (ddq, self.nv, "ddq"), (tau, self.nj, "tau"),
+                              (ee_force, 3 * self.n_contact, "ee_force"), (cnt, self.n_contact, "contact")):
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+            if a.ndim == 1:
+                a = a.reshape(-1, 1)
+            if a.shape[0] != rows:
+                raise ValueError(f"{name}: expected {rows} channels, got shape {a.shape}")
+            ins.append(a)
+        N = ins[0].shape[1]
+        for a in ins:
+            if a.shape[1] != N:
+                raise ValueError("all inputs must have the same number of samples")
+        Y = np.empty((N * self.nv, self.wy))
+        F = np.empty(N * self.nv)
+        self._check(self.lib.sysid_build_full(self._h, *[_ptr(a) for a in ins], N, N, _ptr(Y), _ptr(F)))
+        return Y, F
 
     def tau_error(self, q, dq, ddq, tau, cnt, phi) -> np.ndarray:
         """Sum over samples of the squared torque-prediction error of every row (nv,), K4 on the device."""

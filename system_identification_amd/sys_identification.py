@@ -118,7 +118,20 @@ class SystemIdentification(object):
         self._cache_key, self._cache = (key, tkey), out
         return out
 
-    # ---- per-sample reference API (src/sys_identification.py:401-418) ------------------------
+    # ---- per-sample reference API (src/sys_identification.py:391-418) ------------------------
+    def get_full_regressor_force(self, q, dq, ddq, tau, ee_force, cnt):
+        """Y @ phi = F for the floating-base dynamics M ddq + h = Sᵀ tau + J_cᵀ lambda (:391-399); 1-D inputs
+        give one sample like the reference, channel-major 2-D inputs a stacked batch."""
+        m = self.model
+        q = self._as_channels(q, m.nq, "q")
+        N = q.shape[1]
+        tau = self._as_channels(tau, m.nj, "tau") if m.nj else np.zeros((0, N))
+        cnt = self._as_channels(cnt, m.n_ee, "contact") if m.n_ee else np.zeros((0, N))
+        f = self._as_channels(ee_force, 3 * m.n_ee, "ee_force") if m.n_ee else np.zeros((0, N))
+        dq = self._as_channels(dq, m.nv, "dq")
+        ddq = self._as_channels(ddq, m.nv, "ddq")
+        return self.engine.build_full(q, dq, ddq, tau, f, cnt)
+
     def get_proj_regressor_torque(self, q, dq, ddq, tau, cnt):
         out = self.build_stacked(q, dq, ddq, tau, cnt, _engine.EMIT_Y | _engine.EMIT_TAU)
         return out["Y_proj"], out["tau_proj"]

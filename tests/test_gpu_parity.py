@@ -250,6 +250,31 @@ def test_reduced_precision_gram(robot, N):
     assert np.array_equal(out["f32"], out["f32"].T) and np.array_equal(out["bf16"], out["bf16"].T)
 
 
+@pytest.mark.parametrize("robot,N,cfg", [("solo12", 48, 0), ("spot", 64, 1), ("g1_29dof", 24, 2)])
+def test_full_regressor_force_vs_oracle(robot, N, cfg):
+    """get_full_regressor_force (:391-399) batched on the GPU against the oracle, per sample; LOST=2 values
+    (whose lambda/J_c shapes disagree in the reference) are rejected."""
+    from system_identification_amd.sys_identification import SystemIdentification
+    model = load_robot(robot)
+    d = generate(model, N, config_index=cfg)
+    cnt = np.minimum(d["contact"], 1.0)
+    f = np.random.default_rng(cfg).standard_normal((3 * model.n_ee, N)) * 50.0
+    s = SystemIdentification(robot, None, floating_base=True)
+    Y, F = s.get_full_regressor_force(d["q"], d["dq"], d["ddq"], d["tau"], f, cnt)
+    nv = model.nv
+    for k in range(N):
+        Yr, Fr = ref.get_full_regressor_force(model, d["q"][:, k], d["dq"][:, k], d["ddq"][:, k], d["tau"][:, k],
+                                              f[:, k], cnt[:, k])
+        assert rel(Y[k * nv:(k + 1) * nv], Yr) < TOL
+        assert rel(F[k * nv:(k + 1) * nv], Fr) < TOL
+    Y1, F1 = s.get_full_regressor_force(d["q"][:, 0], d["dq"][:, 0], d["ddq"][:, 0], d["tau"][:, 0], f[:, 0], cnt[:, 0])
+    assert np.array_equal(Y1, Y[:nv]) and np.array_equal(F1, F[:nv])
+    bad = cnt.copy()
+    bad[0, 0] = 2.0
+    with pytest.raises(ValueError):
+        s.get_full_regressor_force(d["q"], d["dq"], d["ddq"], d["tau"], f, bad)
+
+
 def test_rccl_gram_allreduce_single_rank():
     """sysid_allreduce_gram over a one-rank RCCL communicator is the identity on the Gram (the N > 1 path
     needs more GPUs than a test box has; its host logic is covered by the gloo tests)."""

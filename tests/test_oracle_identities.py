@@ -157,3 +157,27 @@ def test_projected_regressor_explains_projected_torque(robot):
     P = ref.null_space_projector(m, d, cnt)
     expect = P @ np.concatenate([resid_base, np.zeros(m.nj)])
     assert np.abs(Yp @ m.phi_pin() - tp - expect).max() < 1e-9 * max(1, np.abs(tau_full).max())
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_full_regressor_force_balances_dynamics(robot):
+    """get_full_regressor_force (:391-399): Y·phi == F = Sᵀtau + J_cᵀlambda when tau and the foot forces come
+    from the same dynamics; lambda follows :137-146 (only feet in contact, in foot order)."""
+    m = load_robot(robot)
+    rng = np.random.default_rng(9)
+    q, v, a = random_state(m, rng)
+    tau_full = inverse_dynamics(m, q[None], v[None], a[None])[0]
+    d = ref.forward_pass(m, q, v, a)
+    cnt = np.zeros(m.n_ee)
+    cnt[0] = 1.0
+    Jc = ref.compute_J_c(m, d, cnt)
+    bd = m.base_dof
+    lam = np.linalg.lstsq(Jc[:, :bd].T, tau_full[:bd], rcond=None)[0]
+    ee_force = np.zeros(3 * m.n_ee)
+    ee_force[:3] = lam
+    ee_force[3:] = rng.standard_normal(3 * m.n_ee - 3)  # forces of feet off the ground are ignored
+    tau = (tau_full - Jc.T @ lam)[bd:]
+    Y, F = ref.get_full_regressor_force(m, q, v, a, tau, ee_force, cnt)
+    assert Y.shape == (m.nv, 10 * m.nb) and F.shape == (m.nv,)
+    resid = np.concatenate([(tau_full - Jc.T @ lam)[:bd], np.zeros(m.nj)])
+    assert np.abs(Y @ m.phi_pin() - F - resid).max() < 1e-9 * max(1, np.abs(tau_full).max())
