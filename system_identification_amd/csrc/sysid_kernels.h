@@ -63,6 +63,10 @@ __host__ __device__ inline int k1_row_groups(int NJ) {
   return 64 / nb > 1 ? 64 / nb : 1;
 }
 
+// Joint records in LDS are padded to 26 doubles (52 dwords): the 24-double stride put bodies i and i+4 on
+// the same LDS banks (4-way conflicts when the lanes of the column phase read 13 different bodies).
+constexpr int BODY_STRIDE = 26;
+
 // Per-wave LDS region of K1 (doubles, every piece 16-B aligned).  W, Pt, pf (dead once J_c is built)
 // and Z (dead once P is built) share one region.
 struct WLay {
@@ -75,7 +79,7 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc)
   int o = 0;
   auto take = [&](int n) { const int r = o; o += (n + 1) & ~1; return r; };
   l.in = take(in_rows);
-  l.body = take(NJ * 24);       // per joint: oR(9) ot(3) v(6) a_gf(6)
+  l.body = take(NJ * BODY_STRIDE);  // per joint: oR(9) ot(3) v(6) a_gf(6), padded
   l.Jw = take(nv * 6);          // spatial axis of every dof [linear at origin; angular]
   l.H1 = take(nv * 6);          // P[:, ff] J_w[:, ff]^T
   l.tp = take(nv);              // P S^T tau
@@ -383,7 +387,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         axis_rotation(axis + 3 * j, q[iq], RJ);
         tJ[0] = tJ[1] = tJ[2] = 0.0;
       }
-      double* bj = body + 24 * j;
+      double* bj = body + BODY_STRIDE * j;
       double tmp[3];
       mat3mul(R0 + 9 * j, RJ, bj);
       mat3vec(R0 + 9 * j, tJ, tmp);
@@ -396,8 +400,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         if (depth[j] != lvl) continue;
         const int p = parent[j];
         const int iv = idx_v[j];
-        const double* bp = body + 24 * p;
-        double* bj = body + 24 * j;
+        const double* bp = body + BODY_STRIDE * p;
+        double* bj = body + BODY_STRIDE * j;
         double liR[9], lit[3], vJ[6], Sa[6];
 #pragma unroll
         for (int k = 0; k < 9; ++k) liR[k] = bj[k];
@@ -456,7 +460,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       if (e < nv) {
         const int r = e;
         const int j = dof_joint[r];
-        const double* bj = body + 24 * j;
+        const double* bj = body + BODY_STRIDE * j;
         double W[3], P[3] = {bj[9], bj[10], bj[11]};
         bool lin = false;
         if (jtype[j] == JT_FREEFLYER) {
@@ -479,7 +483,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
       } else {
         const int c = e - nv;
-        const double* bj = body + 24 * cjoint[c];
+        const double* bj = body + BODY_STRIDE * cjoint[c];
         double x[3];
         mat3vec(bj, ct + 3 * c, x);
         pfs[3 * c] = x[0] + bj[9]; pfs[3 * c + 1] = x[1] + bj[10]; pfs[3 * c + 2] = x[2] + bj[11];
@@ -659,7 +663,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       const int g = it / nbody, i = it - g * nbody + 1;
       const int r0 = g * nv / kp.rg, r1 = (g + 1) * nv / kp.rg;
       double F[FBLK];
-      body_regressor_block(body + 24 * i, F);
+      body_regressor_block(body + BODY_STRIDE * i, F);
       const int cl = chain_len[i];
       int dof[MAXCH <= 4 ? MAXCH : 1];  // short chains: dofs read once, a row's loads issue together
       if constexpr (MAXCH <= 4) {
