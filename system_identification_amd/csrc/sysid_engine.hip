@@ -109,9 +109,12 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
   return SYSID_OK;
 }
 
-// K1 instantiations: chain slots x compile-time nv (quadrupeds: nv = 18; anything else reads nv at
-// run time — a compile-time nv = 35 for the humanoid ran 1.8x slower, its unrolled serial phases
-// being heavier than the saved address arithmetic).
+// K1 instantiations: chain slots x compile-time nv x samples per wave.  Quadrupeds (nv = 18) run two
+// samples per wave; anything else one, with nv read at run time (a compile-time nv = 35 for the humanoid
+// ran 1.8x slower, its unrolled serial phases being heavier than the saved address arithmetic).
+#ifndef SYSID_K1_SPW_QUAD
+#define SYSID_K1_SPW_QUAD 2
+#endif
 enum { K1_C4_NV18, K1_C4, K1_C16 };
 
 int k1_variant(int maxch_tpl, int nv) {
@@ -119,11 +122,13 @@ int k1_variant(int maxch_tpl, int nv) {
   return K1_C16;
 }
 
+int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : 1; }
+
 const void* k1_fn(int variant) {
   switch (variant) {
-    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<4, 18>);
-    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0>);
-    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0>);
+    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<4, 18, SYSID_K1_SPW_QUAD>);
+    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, 1>);
+    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, 1>);
   }
 }
 
@@ -134,22 +139,24 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
     kp.full = 1;
     kp.in_rows = e->in_lds;
   }
+  const int spw = k1_spw(e->k1_variant);
+  kp.rg = k1_row_groups(kp.NJ, 64 / spw);
   kp.out_cols = (int)std::min<int64_t>(ld_panel, e->ldp);
-  const int64_t waves_needed = N;
+  const int64_t waves_needed = (N + spw - 1) / spw;
   const int64_t cap = (int64_t)e->cus * e->k1_blocks_per_cu;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + e->k1_waves - 1) / e->k1_waves));
   const dim3 g1((unsigned)grid), b1(64 * e->k1_waves);
   switch (e->k1_variant) {
     case K1_C4_NV18:
-      hipLaunchKernelGGL((k1_regressor_panel<4, 18>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
-                         ld_panel, e->d_work, dbg);
+      hipLaunchKernelGGL((k1_regressor_panel<4, 18, SYSID_K1_SPW_QUAD>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N,
+                         ld, d_panel, ld_panel, e->d_work, dbg);
       break;
     case K1_C4:
-      hipLaunchKernelGGL((k1_regressor_panel<4, 0>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+      hipLaunchKernelGGL((k1_regressor_panel<4, 0, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
                          ld_panel, e->d_work, dbg);
       break;
     default:
-      hipLaunchKernelGGL((k1_regressor_panel<16, 0>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+      hipLaunchKernelGGL((k1_regressor_panel<16, 0, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
                          ld_panel, e->d_work, dbg);
   }
   HIP_TRY(e, hipGetLastError());
@@ -408,7 +415,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
   kp.in_lds = in_lds; kp.full = 0;
   kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL.total; kp.out_cols = e->ldp;
-  kp.rg = k1_row_groups(NJ);
+  kp.rg = k1_row_groups(NJ, 64);  // per launch: k1_row_groups(NJ, lanes per sample)
   kp.thr_rel = 1e-13;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;
@@ -453,7 +460,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) {
     int best = -1;
     for (int wv : {4, 2, 1}) {
-      const size_t lds = (size_t)(MI.ndbl + wv * WL.total) * sizeof(double);
+      const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(e->k1_variant) * WL.total) * sizeof(double);
       if (lds > 160 * 1024) continue;
       (void)hipFuncSetAttribute(k1_fn(e->k1_variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       int nb = 0;

@@ -57,10 +57,10 @@ __host__ __device__ inline MImg mimg_layout(int NJ, int nv, int nc, int maxch) {
   return m;
 }
 
-// Row groups of K1's regressor-column phase: lanes = bodies x row groups, one pass of 64 lanes.
-__host__ __device__ inline int k1_row_groups(int NJ) {
+// Row groups of K1's regressor-column phase: lanes = bodies x row groups, one pass of a sample's lanes.
+__host__ __device__ inline int k1_row_groups(int NJ, int lanes) {
   const int nb = NJ - 1 > 0 ? NJ - 1 : 1;
-  return 64 / nb > 1 ? 64 / nb : 1;
+  return lanes / nb > 1 ? lanes / nb : 1;
 }
 
 // Joint records in LDS are padded to 26 doubles (52 dwords): the 24-double stride put bodies i and i+4 on
@@ -276,7 +276,10 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 // ------------------------------------------------------------------------------------------------
 // MAXCH: chain-slot count (>= longest revolute chain).  NVC: nv fixed at compile time (0 = read it
 // from K1Params), so the row loops of the common robots unroll with immediate LDS offsets.
-template <int MAXCH, int NVC>
+// SPW: samples per wave (1 or 2).  With SPW > 1 each 64/SPW-lane slice of the wave carries its own
+// sample through every phase, so the lane-starved serial phases (forward pass, exchange steps) do SPW
+// samples per instruction; each slice has its own LDS region.
+template <int MAXCH, int NVC, int SPW>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
 #endif
@@ -312,8 +315,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const int nv = NVC > 0 ? NVC : kp.nv;
   const int nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  static_assert(SPW == 1 || SPW == 2, "1 or 2 samples per wave (4 measured 34% slower)");
+  constexpr int HW = 64 / SPW;                       // lanes per sample
+  const int half = lane / HW, hl = lane % HW;         // sample slot within the wave, lane within it
   const WLay L = wave_layout(kp.in_lds, nv, NJ, nc);
-  double* wr = smem + kp.mimg_dbl + wave * kp.wave_dbl;
+  double* wr = smem + kp.mimg_dbl + (wave * SPW + half) * kp.wave_dbl;
   double* body = wr + L.body;
   double* Ws = wr + L.W;
   double* Pts = wr + L.Pt;
@@ -325,23 +331,27 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   double* H1 = wr + L.H1;
   double* tps = wr + L.tp;
 
-  // Samples are handed out one at a time from a device counter (work[0]), so a workgroup that becomes
-  // resident late, or a slow CU, only ever costs its own last sample.  The next index is claimed one
-  // sample ahead, its inputs are prefetched into registers (channel c -> lane c, c+64, c+128) while the
-  // current sample runs.  The last wave to leave resets the counters for the next launch (work[1]
-  // counts departed waves; no wave touches work[0] after its last claim returned >= N).
+  // Samples are handed out SPW at a time from a device counter (work[0]), so a workgroup that becomes
+  // resident late, or a slow CU, only ever costs its own last samples.  The next ones are claimed one
+  // step ahead and their inputs prefetched into registers (channel c -> lane c, c+HW, ...) while the
+  // current ones run.  The last wave to leave resets the counters for the next launch (work[1] counts
+  // departed waves; no wave touches work[0] after its last claim returned >= N).
   auto claim = [&]() -> int64_t {
     unsigned long long v = 0;
-    if (lane == 0) v = atomicAdd(work, 1ull);
+    if (lane == 0) v = atomicAdd(work, (unsigned long long)SPW);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return (int64_t)(((unsigned long long)hi << 32) | lo);
   };
-  double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-  auto fetch = [&](int64_t s) {
-    if (lane < IN) x0 = in[(int64_t)lane * ld + s];
-    if (lane + 64 < IN) x1 = in[(int64_t)(lane + 64) * ld + s];
-    if (lane + 128 < IN) x2 = in[(int64_t)(lane + 128) * ld + s];
+  constexpr int NXR = (192 + HW - 1) / HW;  // input registers per lane (<= 192 channels)
+  double xr[NXR];
+#pragma unroll
+  for (int u = 0; u < NXR; ++u) xr[u] = 0.0;
+  auto fetch = [&](int64_t s) {  // s = the step's first sample; this half's is s + half
+    const int64_t sh = s + half;
+#pragma unroll
+    for (int u = 0; u < NXR; ++u)
+      if (hl + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hl + HW * u) * ld + sh];
   };
   double* sin_ = wr + L.in;
   const double* q = sin_;
@@ -359,17 +369,18 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #endif
 
   while (s < N) {
+    const bool valid = s + half < N;  // the step's last samples may not exist
     wsync();
-    if (lane < IN) sin_[lane] = x0;
-    if (lane + 64 < IN) sin_[lane + 64] = x1;
-    if (lane + 128 < IN) sin_[lane + 128] = x2;
-    const int64_t s2 = s1 < N ? claim() : N;  // used one sample from now
+#pragma unroll
+    for (int u = 0; u < NXR; ++u)
+      if (hl + HW * u < IN) sin_[hl + HW * u] = xr[u];
+    const int64_t s2 = s1 < N ? claim() : N;  // used one step from now
     if (s1 < N) fetch(s1);
-    if (lane < 24) {
+    for (int x = hl; x < 24; x += HW) {
       double v = 0.0;
-      if (lane == 0 || lane == 4 || lane == 8) v = 1.0;   // oR_0 = I
-      if (lane >= 18 && lane < 21) v = -(lane == 18 ? kp.g0 : (lane == 19 ? kp.g1 : kp.g2));
-      body[lane] = v;
+      if (x == 0 || x == 4 || x == 8) v = 1.0;   // oR_0 = I
+      if (x >= 18 && x < 21) v = -(x == 18 ? kp.g0 : (x == 19 ? kp.g1 : kp.g2));
+      body[x] = v;
     }
     wsync();
     K1_STAMP(0)
@@ -377,7 +388,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // ---- forward pass (computeJointTorqueRegressor forward step) + placements ----
     // Joint placements liMi = jointPlacement * M_J(q) of every joint at once (one lane per joint: the
     // sincos / quaternion work is off the depth-serial path), parked in the joint's own pose slot.
-    for (int j = 1 + lane; j < NJ; j += 64) {
+    for (int j = 1 + hl; j < NJ; j += HW) {
       const int iq = idx_q[j];
       double RJ[9], tJ[3];
       if (jtype[j] == JT_FREEFLYER) {
@@ -396,7 +407,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     // Velocities / accelerations level by level (a joint's parent is one level up).
     for (int lvl = 1; lvl <= kp.maxdepth; ++lvl) {
-      for (int j = 1 + lane; j < NJ; j += 64) {
+      for (int j = 1 + hl; j < NJ; j += HW) {
         if (depth[j] != lvl) continue;
         const int p = parent[j];
         const int iv = idx_v[j];
@@ -456,7 +467,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     K1_STAMP(1)
 
     // ---- world motion axes of every dof; contact points ----
-    for (int e = lane; e < nv + nc; e += 64) {
+    for (int e = hl; e < nv + nc; e += HW) {
       if (e < nv) {
         const int r = e;
         const int j = dof_joint[r];
@@ -496,7 +507,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     K1_STAMP(2)
 
     // ---- contact Jacobian (LOCAL_WORLD_ALIGNED, linear rows) ----
-    for (int e = lane; e < k * nv; e += 64) {
+    for (int e = hl; e < k * nv; e += HW) {
       const int rho = e / nv, r = e - rho * nv;
       int c = 0;
       for (int seen = -1; c < nc; ++c) {  // the (rho/3)-th contact with a non-zero value
@@ -524,7 +535,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 
     if (kp.full) {
       // get_full_regressor_force (src/sys_identification.py:391-399): no projection
-      for (int e = lane; e < nv * nv; e += 64) {
+      for (int e = hl; e < nv * nv; e += HW) {
         const int a = e / nv;
         Ps[e] = e - a * nv == a ? 1.0 : 0.0;
       }
@@ -532,7 +543,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     } else {
       // ---- M = J_c J_c^T, into the exchange buffer that makes the k ping-pong steps end in Ms ----
       double* M0 = (k & 1) ? wr + L.M2 : Ms;
-      for (int e = lane; e < k * k; e += 64) {
+      for (int e = hl; e < k * k; e += HW) {
         const int a = e / k, b = e - a * k;
         double acc = 0.0;
 #pragma unroll 6
@@ -558,12 +569,12 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         for (int j = 0; j < k; ++j) {
           const double pj = src[j * k + j];
           // three entries per lane per pass: all their loads issue before any store of the pass
-          for (int e0 = lane; e0 < k * k; e0 += 192) {
+          for (int e0 = hl; e0 < k * k; e0 += 3 * HW) {
             int r[3], c[3];
             double arc[3], arj[3], ajc[3];
 #pragma unroll
             for (int u = 0; u < 3; ++u) {
-              const int e = e0 + 64 * u;
+              const int e = e0 + HW * u;
               const int ee = e < k * k ? e : 0;
               r[u] = (int)(((float)ee + 0.5f) * rk);  // exact: ee < 24*24
               c[u] = ee - r[u] * k;
@@ -576,7 +587,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
             for (int u = 0; u < 3; ++u) {
               const double v = r[u] == j ? (c[u] == j ? ip : ajc[u] * ip)
                                          : (c[u] == j ? -arj[u] * ip : arc[u] - arj[u] * ajc[u] * ip);
-              if (e0 + 64 * u < k * k) dst[e0 + 64 * u] = v;
+              if (e0 + HW * u < k * k) dst[e0 + HW * u] = v;
             }
           }
           wsync();
@@ -590,7 +601,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 
       // ---- Z = X J_c ;  P = I - J_c^T Z ----
       double* Zs = wr + L.Z;
-      for (int e = lane; e < k * nv; e += 64) {
+      for (int e = hl; e < k * nv; e += HW) {
         const int a = e / nv, r = e - a * nv;
         double acc = 0.0;
 #pragma unroll 4
@@ -598,7 +609,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         Zs[e] = acc;
       }
       wsync();
-      for (int e = lane; e < nv * nv; e += 64) {
+      for (int e = hl; e < nv * nv; e += HW) {
         const int a = e / nv, b = e - a * nv;
         double acc = 0.0;
 #pragma unroll 4
@@ -610,7 +621,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     K1_STAMP(5)
 
     // ---- H1 = P[:, ff] J_w[:, ff]^T ;  tp = P S^T tau ----
-    for (int e = lane; e < nv * 7; e += 64) {
+    for (int e = hl; e < nv * 7; e += HW) {
       if (e < nv * 6) {
         const int r = e / 6, c = e - 6 * r;
         double h = 0.0;
@@ -637,7 +648,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
             if (comp == 0)
               for (++c; c < nc && cnt[c] == 0.0; ++c) {}
             const double* lw = lam + 3 * c;
-            const double lb = Rb[comp] * lw[0] + Rb[3 + comp] * lw[1] + Rb[6 + comp] * lw[2];
+            // column `comp` of R_b by selects (a dynamic index would put Rb in scratch memory)
+            const double c0 = comp == 0 ? Rb[0] : (comp == 1 ? Rb[1] : Rb[2]);
+            const double c1 = comp == 0 ? Rb[3] : (comp == 1 ? Rb[4] : Rb[5]);
+            const double c2 = comp == 0 ? Rb[6] : (comp == 1 ? Rb[7] : Rb[8]);
+            const double lb = c0 * lw[0] + c1 * lw[1] + c2 * lw[2];
             acc += Jc[rho * nv + r] * lb;
           }
         }
@@ -645,9 +660,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
     }
     wsync();
-    if (dbg != nullptr && s == 0) {
+    if (dbg != nullptr && s + half == 0) {
 #ifndef SYSID_STAMPS
-      for (int x = lane; x < L.total; x += 64) dbg[x] = wr[x];  // diagnostics: LDS image of sample 0
+      for (int x = hl; x < L.total; x += HW) dbg[x] = wr[x];  // diagnostics: LDS image of sample 0
 #endif
     }
     K1_STAMP(6)
@@ -657,9 +672,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
     // One G row (6 + 6*chain FMAs) feeds 42 FMAs and five 16-byte stores.  (Staging the rows through
     // LDS to make the stores contiguous measured 17% slower: the store path is not the limiter.)
-    double* out = panel + (s * nv) * ldp;
+    double* out = panel + ((s + half) * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
-    for (int it = lane; it < nyi; it += 64) {
+    for (int it = hl; it < nyi && valid; it += HW) {
       const int g = it / nbody, i = it - g * nbody + 1;
       const int r0 = g * nv / kp.rg, r1 = (g + 1) * nv / kp.rg;
       double F[FBLK];
@@ -713,7 +728,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // ---- [B_v | B_c | tau_proj | pad]: lane = (row, column pair), 16-byte stores ----
     {
       const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
-      for (int it = lane; it < nv * npair; it += 64) {
+      for (int it = hl; it < nv * npair && valid; it += HW) {
         const int r = it / npair, m = it - r * npair;
         const double* pr = Ps + r * nv + bd;
         double v2[2];
