@@ -115,6 +115,9 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
 #ifndef SYSID_K1_SPW_QUAD
 #define SYSID_K1_SPW_QUAD 2
 #endif
+#ifndef SYSID_K1_SPW_GEN
+#define SYSID_K1_SPW_GEN 1
+#endif
 enum { K1_C4_NV18, K1_C4, K1_C16 };
 
 int k1_variant(int maxch_tpl, int nv) {
@@ -122,13 +125,13 @@ int k1_variant(int maxch_tpl, int nv) {
   return K1_C16;
 }
 
-int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : 1; }
+int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : SYSID_K1_SPW_GEN; }
 
 const void* k1_fn(int variant) {
   switch (variant) {
     case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<4, 18, SYSID_K1_SPW_QUAD>);
-    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, 1>);
-    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, 1>);
+    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN>);
+    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN>);
   }
 }
 
@@ -152,11 +155,11 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
                          ld, d_panel, ld_panel, e->d_work, dbg);
       break;
     case K1_C4:
-      hipLaunchKernelGGL((k1_regressor_panel<4, 0, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+      hipLaunchKernelGGL((k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
                          ld_panel, e->d_work, dbg);
       break;
     default:
-      hipLaunchKernelGGL((k1_regressor_panel<16, 0, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+      hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
                          ld_panel, e->d_work, dbg);
   }
   HIP_TRY(e, hipGetLastError());
