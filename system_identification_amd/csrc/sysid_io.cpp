@@ -13,6 +13,7 @@
 #include <charconv>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -151,7 +152,11 @@ bool parse_span(const char* b, const char* e, int64_t count, float* out) {
       continue;
     }
     const auto r = std::from_chars(s, te, v);
-    if (r.ec != std::errc() || r.ptr != te) {
+    if (r.ec == std::errc::result_out_of_range && r.ptr == te) {
+      // overflow / underflow: Python's float() gives +-inf / +-0 (strtod's HUGE_VAL / 0 with ERANGE)
+      std::string f(p, te);
+      v = std::strtod(f.c_str(), nullptr);
+    } else if (r.ec != std::errc() || r.ptr != te) {
       // inf / nan spellings accepted by np.loadtxt
       std::string f(p, te);
       std::transform(f.begin(), f.end(), f.begin(), [](unsigned char c) { return (char)std::tolower(c); });

@@ -180,3 +180,16 @@ def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_typ
     if prob.status in (cp.OPTIMAL, cp.OPTIMAL_INACCURATE):
         return phi.value
     raise ValueError("The problem did not solve to optimality.")
+
+
+# ---- checkpoint of the normal equations (the Gram is tiny; resume the SDP without the data) --
+def save_normal_equations(path, ne: dict) -> None:
+    """Write {gram, Atb, btb, num_rows} to an .npz (plain arrays, no pickle)."""
+    np.savez(path, gram=np.asarray(ne["gram"], dtype=np.float64), Atb=np.asarray(ne["Atb"], dtype=np.float64),
+             btb=np.float64(ne["btb"]), num_rows=np.int64(ne["num_rows"]))
+
+
+def load_normal_equations(path) -> dict:
+    with np.load(path, allow_pickle=False) as z:
+        return {"gram": z["gram"].copy(), "Atb": z["Atb"].copy(), "btb": float(z["btb"]),
+                "num_rows": int(z["num_rows"])}

@@ -72,3 +72,47 @@ def test_native_dat_reader_matches_loadtxt(tmp_path):
         load_dat(bad)
     with pytest.raises(ValueError):
         load_dat(tmp_path / "missing.dat")
+
+
+def test_dat_reader_under_address_sanitizer(tmp_path):
+    """The native reader compiled for the host with -fsanitize=address,undefined parses good files to the
+    same sums as np.loadtxt and rejects malformed ones cleanly (no sanitizer report, exit code 0)."""
+    import os
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "asan"
+    subprocess.run([gxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-I" + os.path.join(root, "include"), "-o", str(exe),
+                    os.path.join(root, "tests", "native", "dat_reader_asan.cpp"),
+                    os.path.join(root, "system_identification_amd", "csrc", "sysid_io.cpp"), "-lpthread"],
+                   check=True, timeout=240)
+    rng = np.random.default_rng(3)
+    good = tmp_path / "good.dat"
+    a = rng.standard_normal((7, 5003)).astype(np.float32)
+    np.savetxt(good, a, delimiter="\t", fmt="%.9g")
+    files = {"good": good}
+    for name, text in (("ragged", "1\t2\t3\n4\t5\n"), ("junk", "1\tx\t3\n"), ("empty", ""), ("blank", "\n\n"),
+                       ("trailing_tab", "1\t2\t\n"), ("crlf", "1\t2\r\n3\t4\r\n"), ("long", "1e999\t-0\t.5\n")):
+        p = tmp_path / f"{name}.dat"
+        p.write_text(text)
+        files[name] = p
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    res = subprocess.run([str(exe)] + [str(p) for p in files.values()], capture_output=True, text=True, env=env,
+                         timeout=120)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert "ERROR: AddressSanitizer" not in res.stderr and "runtime error" not in res.stderr, res.stderr[-2000:]
+    out = dict(zip(files, res.stdout.split("\n")))
+    r, c, rc, s = out["good"].split()
+    ref = np.loadtxt(good, delimiter="\t", dtype=np.float32)
+    assert (int(r), int(c), int(rc)) == (7, 5003, 0)
+    assert abs(float(s) - float(ref.astype(np.float64).sum())) < 1e-6 * np.abs(ref).sum()
+    for bad in ("ragged", "junk", "trailing_tab"):
+        assert int(out[bad].split()[2]) != 0
+    assert out["crlf"].split()[:3] == ["2", "2", "0"]
+    assert out["long"].split()[:3] == ["1", "3", "0"] and out["long"].split()[3] == "inf"  # float('1e999') = inf
+    assert out["empty"].split()[:3] == ["0", "0", "0"]

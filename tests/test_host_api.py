@@ -91,3 +91,14 @@ def test_shape_errors_are_value_errors():
     s = SystemIdentification("spot")
     with pytest.raises(ValueError):
         s.build_stacked(np.zeros((18, 3)), np.zeros((18, 3)), np.zeros((18, 3)), np.zeros((12, 3)), np.zeros((4, 3)))
+
+
+def test_normal_equations_checkpoint_round_trip(tmp_path):
+    from system_identification_amd.solver import load_normal_equations, save_normal_equations
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((40, 7))
+    ne = {"gram": A.T @ A, "Atb": A.T @ A[:, 0], "btb": 3.25, "num_rows": 40}
+    save_normal_equations(tmp_path / "ne.npz", ne)
+    back = load_normal_equations(tmp_path / "ne.npz")
+    assert np.array_equal(back["gram"], ne["gram"]) and np.array_equal(back["Atb"], ne["Atb"])
+    assert back["btb"] == 3.25 and back["num_rows"] == 40
