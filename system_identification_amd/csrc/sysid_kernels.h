@@ -680,11 +680,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       double F[FBLK];
       body_regressor_block(body + BODY_STRIDE * i, F);
       const int cl = chain_len[i];
-      int dof[MAXCH <= 4 ? MAXCH : 1];  // short chains: dofs read once, a row's loads issue together
-      if constexpr (MAXCH <= 4) {
+      int dof[MAXCH];  // the chain's dofs, read once: no dependent index load per row
 #pragma unroll
-        for (int t = 0; t < MAXCH; ++t) dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
-      }
+      for (int t = 0; t < MAXCH; ++t) dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
       double* oi = out + 10 * (i - 1);
       for (int r = r0; r < r1; ++r) {
         const double* h = H1 + 6 * r;
@@ -692,21 +690,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         double G[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) G[k] = h[k];
-        if constexpr (MAXCH <= 4) {
 #pragma unroll
-          for (int t = 0; t < MAXCH; ++t) {
-            if (t < cl) {
-              const double pv = pr[dof[t]];
-              const double* jw = Jws + 6 * dof[t];
-#pragma unroll
-              for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
-            }
-          }
-        } else {
-          for (int t = 0; t < cl; ++t) {
-            const int d = chain[i * kp.maxch + t];
-            const double pv = pr[d];
-            const double* jw = Jws + 6 * d;
+        for (int t = 0; t < MAXCH; ++t) {
+          if (t < cl) {
+            const double pv = pr[dof[t]];
+            const double* jw = Jws + 6 * dof[t];
 #pragma unroll
             for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
           }
