@@ -44,7 +44,7 @@ def test_projector_identities(robot, seed):
     d = ref.forward_pass(m, q, v, a)
     Jc = ref.compute_J_c(m, d, cnt)
     P = ref.null_space_projector(m, d, cnt)
-    assert np.abs(P @ Jc.T).max() < 1e-10
+    assert np.abs(P @ Jc.T).max(initial=0.0) < 1e-10
     assert np.abs(P @ P - P).max() < 1e-10
     assert np.abs(P - P.T).max() < 1e-10
     if not cnt.any():
