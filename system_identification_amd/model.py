@@ -527,7 +527,7 @@ def build_model_from_urdf(urdf_file: str, config_file: str | None = None,
 # ------------------------------------------------------------------------------------------------
 
 ROBOT_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "robots")
-ROBOTS = ("solo12", "spot", "g1_29dof")
+ROBOTS = ("solo12", "spot", "g1_29dof", "solo12_fixed")
 
 
 def load_robot(name: str) -> Model:

@@ -6,7 +6,7 @@ fixtures or .dat data, so the vectors come from oracle/ref_numpy.py, itself pinn
 and the reference-path outputs: stacked Y_proj, tau_proj, B_v, B_c, the unprojected regressor Y, the
 stacked contact Jacobians, and the normal equations.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [robot ...]
 """
 import os
 import sys
@@ -63,6 +63,9 @@ def make(robot, seed):
     print(f"{robot}: {N} samples -> {path} ({os.path.getsize(path)} B)")
 
 
+ROBOTS = ("solo12", "spot", "g1_29dof", "solo12_fixed")  # seed 1000 + position
+
 if __name__ == "__main__":
-    for k, r in enumerate(("solo12", "spot", "g1_29dof")):
-        make(r, 1000 + k)
+    for k, r in enumerate(ROBOTS):
+        if len(sys.argv) == 1 or r in sys.argv[1:]:
+            make(r, 1000 + k)

@@ -8,9 +8,11 @@ import pytest
 from oracle import ref_numpy as ref
 from system_identification_amd.model import load_robot
 from tests import alg_mirror as am
+from tests.parity import rel as rel_floor
+from tests.parity import unprojected_scales
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-ROBOTS = ["solo12", "spot", "g1_29dof"]
+ROBOTS = ["solo12", "spot", "g1_29dof", "solo12_fixed"]
 
 
 def load(robot):
@@ -45,11 +47,13 @@ def test_kernel_formulation_matches_golden(robot):
     """The HIP kernel's algebra (world axes, exchange-inverse projector, H1 + revolute chain) in numpy."""
     g, m = load(robot), load_robot(robot)
     nv = m.nv
+    scales = unprojected_scales(m, g["q"], g["dq"], g["ddq"], g["tau"])
     for s in range(g["q"].shape[1]):
         Y, t, Bv, Bc = am.sample_panel(m, g["q"][:, s], g["dq"][:, s], g["ddq"][:, s], g["tau"][:, s], g["contact"][:, s])
         sl = slice(s * nv, (s + 1) * nv)
-        for a, b in ((Y, g["Y_proj"][sl]), (t, g["tau_proj"][sl]), (Bv, g["B_v"][sl]), (Bc, g["B_c"][sl])):
-            assert rel(a, b) < 1e-6  # north_star parity bar; (J_c J_c^T)^-1 projector error ~ eps·cond(J_c)^2
+        for a, b, c in zip((Y, t, Bv, Bc), (g["Y_proj"][sl], g["tau_proj"][sl], g["B_v"][sl], g["B_c"][sl]), scales[s]):
+            # north_star parity bar; (J_c J_c^T)^-1 projector error ~ eps·cond(J_c)^2 (floor: tests/parity.py)
+            assert rel_floor(a, b, c) < 1e-6
 
 
 @pytest.mark.parametrize("robot", ROBOTS)

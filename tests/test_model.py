@@ -10,18 +10,23 @@ from system_identification_amd.model import (Model, build_model_from_urdf, load_
                                              JOINT_FREEFLYER)
 from tests.conftest import REFERENCE, needs_reference
 
-SOURCES = {
-    "solo12": ("files/solo_description/solo12.urdf", "files/solo_description/solo12_config.yaml"),
-    "spot": ("files/spot_description/spot.urdf", "files/spot_description/spot_config.yaml"),
+SOURCES = {  # robot: (urdf, yaml, floating_base)
+    "solo12": ("files/solo_description/solo12.urdf", "files/solo_description/solo12_config.yaml", True),
+    "spot": ("files/spot_description/spot.urdf", "files/spot_description/spot_config.yaml", True),
+    "solo12_fixed": ("files/solo_description/solo12.urdf", "files/solo_description/solo12_config.yaml", False),
 }
 
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_committed_dims(robot):
     m = load_robot(robot)
-    expect = {"solo12": (19, 18, 13, 4), "spot": (19, 18, 13, 4), "g1_29dof": (36, 35, 30, 2)}[robot]
+    expect = {"solo12": (19, 18, 13, 4), "spot": (19, 18, 13, 4), "g1_29dof": (36, 35, 30, 2),
+              "solo12_fixed": (12, 12, 12, 4)}[robot]
     assert (m.nq, m.nv, m.nb, m.n_ee) == expect
-    assert m.jtypes[1] == JOINT_FREEFLYER and m.parents[1] == 0
+    if m.floating_base:
+        assert m.jtypes[1] == JOINT_FREEFLYER and m.parents[1] == 0
+    else:
+        assert JOINT_FREEFLYER not in list(m.jtypes) and m.base_dof == 0
     # DFS numbering: a parent always precedes its children
     assert all(m.parents[i] < i for i in range(1, m.njoints))
 
@@ -29,8 +34,8 @@ def test_committed_dims(robot):
 @needs_reference
 @pytest.mark.parametrize("robot", list(SOURCES))
 def test_committed_json_is_fresh(robot):
-    u, c = SOURCES[robot]
-    fresh = build_model_from_urdf(os.path.join(REFERENCE, u), os.path.join(REFERENCE, c))
+    u, c, floating = SOURCES[robot]
+    fresh = build_model_from_urdf(os.path.join(REFERENCE, u), os.path.join(REFERENCE, c), floating_base=floating)
     assert fresh.to_json() == load_robot(robot).to_json()
 
 
@@ -75,9 +80,10 @@ def test_frames_match_independent_urdf_walk(robot):
         os.path.join(REFERENCE, "files/g1_description/g1_29dof.urdf")
     rng = np.random.default_rng(0)
     q = np.zeros(m.nq)
-    q[6] = 1.0  # identity base
+    if m.floating_base:
+        q[6] = 1.0  # identity base
     vals = {}
-    for i in range(2, m.njoints):
+    for i in range(2 if m.floating_base else 1, m.njoints):
         q[m.idx_q[i]] = rng.uniform(-1, 1)
         vals[m.joint_names[i]] = q[m.idx_q[i]]
     d = ref.forward_pass(m, q, np.zeros(m.nv), np.zeros(m.nv))

@@ -7,7 +7,7 @@ from oracle import ref_numpy as ref
 from system_identification_amd.dynamics import inverse_dynamics
 from system_identification_amd.model import load_robot, rpy_to_matrix
 
-ROBOTS = ["solo12", "spot", "g1_29dof"]
+ROBOTS = ["solo12", "spot", "g1_29dof", "solo12_fixed"]
 
 
 def random_state(m, rng, normalise=True):

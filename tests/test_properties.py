@@ -6,11 +6,13 @@ from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
 from tests import alg_mirror as am
+from tests.parity import rel as rel_floor
+from tests.parity import unprojected_scales
 from oracle import ref_numpy as ref
 from system_identification_amd.dynamics import inverse_dynamics
 from system_identification_amd.model import load_robot
 
-MODELS = {r: load_robot(r) for r in ("solo12", "spot", "g1_29dof")}
+MODELS = {r: load_robot(r) for r in ("solo12", "spot", "g1_29dof", "solo12_fixed")}
 robots = st.sampled_from(sorted(MODELS))
 seeds = st.integers(0, 2**32 - 1)
 
@@ -61,5 +63,6 @@ def test_kernel_algebra_matches_oracle(robot, seed):
     Y, t, Bv, Bc = am.sample_panel(m, q, v, a, tau, cnt)
     Yr, tr = ref.get_proj_regressor_torque(m, q, v, a, tau, cnt)
     Bvr, Bcr = ref.get_proj_friction_regressors(m, q, v, a, cnt)
-    for x, r in ((Y, Yr), (t, tr), (Bv, Bvr), (Bc, Bcr)):
-        assert np.abs(x - r).max() <= 1e-6 * max(np.abs(r).max(), 1e-300)
+    sc = unprojected_scales(m, q[:, None], v[:, None], a[:, None], tau[:, None])[0]
+    for x, r, c in zip((Y, t, Bv, Bc), (Yr, tr, Bvr, Bcr), sc):
+        assert rel_floor(x, r, c) <= 1e-6  # fully pinned samples: see tests/parity.py
