@@ -127,6 +127,9 @@ int k1_variant(int maxch_tpl, int nv) {
 
 int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : SYSID_K1_SPW_GEN; }
 
+// wave_layout's `hw`: lanes per sample of the compile-time-nv kernel (P over Z), 0 for the others.
+int k1_layout_hw(int variant) { return variant == K1_C4_NV18 ? 64 / k1_spw(variant) : 0; }
+
 const void* k1_fn(int variant) {
   switch (variant) {
     case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<4, 18, SYSID_K1_SPW_QUAD>);
@@ -412,7 +415,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->ldp = (e->ncol + 1) & ~1;
   e->in_rows = in_rows;
   e->in_lds = in_lds;
-  const WLay WL = wave_layout(in_lds, nv, NJ, nc);
+  e->k1_variant = k1_variant(maxch_tpl, nv);
+  const WLay WL = wave_layout(in_lds, nv, NJ, nc, k1_layout_hw(e->k1_variant));
   K1Params& kp = e->kp;
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
@@ -422,7 +426,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.thr_rel = 1e-13;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;
-  e->k1_variant = k1_variant(maxch_tpl, nv);
 
   // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
   // K2_WAVES x K2_SPW super slots per workgroup group; 4 tile slots per super slot.
@@ -820,7 +823,7 @@ int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6) {
 
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
   if (!e || !offsets12) return SYSID_E_INVALID;
-  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc);
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant));
   const int o[12] = {L.in, L.body, L.W, L.Pt, L.Jw, L.pf, L.Jc, L.M, L.P, L.H1, L.tp, L.total};
   for (int k = 0; k < 12; ++k) offsets12[k] = o[k];
   return SYSID_OK;
@@ -829,7 +832,7 @@ int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
 int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
                         const double* cnt, double* lds_image, int64_t image_doubles) {
   if (!e || !lds_image) return set_err(e, SYSID_E_INVALID, "null argument");
-  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc);
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant));
   if (image_doubles < L.total) return set_err(e, SYSID_E_INVALID, "image needs %d doubles", L.total);
   HIP_TRY(e, hipSetDevice(e->device));
   int rc = sysid_build(e, q, dq, ddq, tau, cnt, 1, 1, SYSID_EMIT_Y, nullptr, nullptr, nullptr, nullptr, nullptr,

@@ -67,33 +67,56 @@ __host__ __device__ inline int k1_row_groups(int NJ, int lanes) {
 // the same LDS banks (4-way conflicts when the lanes of the column phase read 13 different bodies).
 constexpr int BODY_STRIDE = 26;
 
-// Per-wave LDS region of K1 (doubles, every piece 16-B aligned).  W, Pt, pf (dead once J_c is built)
-// and Z (dead once P is built) share one region.
+// Per-wave LDS region of K1 (doubles, every piece 16-B aligned).  The projector's working set
+// D = [J_c | M | W,Pt,pf / M2 / Z] is dead once P is built, and holds its results too:
+//   * H1 over J_c (stored after the tau column, which reads J_c in the full mode), or after everything
+//     when J_c's slot is smaller;
+//   * with `hw` > 0 (lanes per sample of a compile-time-nv kernel) P ends inside Z's slot: P is built
+//     row-major, `hw` entries per wave pass, row a from Z row a (Z is stored transposed, stride 3 nc), so
+//     a pass may overwrite the Z rows the passes before it consumed; P starts `margin` doubles before Z,
+//     the largest lead of the written entries over the consumed Z rows (over M, dead after Z is built).
+//     Spot: 1,582 -> 1,158 doubles per sample, so 8 two-sample waves share a CU's 160 KB (was 6).
+//   * otherwise P follows D.
 struct WLay {
-  int in, body, W, Pt, Jw, pf, Jc, M, M2, P, H1, tp, Z, total;
+  int in, body, W, Pt, Jw, pf, Jc, M, M2, P, H1, tp, dqs, Z, total;
 };
 
-__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc) {
+__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc, int hw) {
   WLay l;
   const int k = 3 * nc;
   int o = 0;
-  auto take = [&](int n) { const int r = o; o += (n + 1) & ~1; return r; };
+  auto r2 = [](int n) { return (n + 1) & ~1; };
+  auto take = [&](int n) { const int r = o; o += r2(n); return r; };
+  auto grow = [&](int end) { if (o < end) o = end; };
   l.in = take(in_rows);
   l.body = take(NJ * BODY_STRIDE);  // per joint: oR(9) ot(3) v(6) a_gf(6), padded
   l.Jw = take(nv * 6);          // spatial axis of every dof [linear at origin; angular]
-  l.H1 = take(nv * 6);          // P[:, ff] J_w[:, ff]^T
   l.tp = take(nv);              // P S^T tau
+  l.dqs = take(nv);             // dq for the friction columns (`in` takes the next sample's inputs mid-step)
+  const int D = o;
+  l.Jc = take(k * nv);          // J_c
+  int margin = 0;
+  if (hw > 0)
+    for (int E = hw; E < nv * nv; E += hw) {
+      const int lead = E - k * (E / nv);
+      if (lead > margin) margin = lead;
+    }
+  l.M = take(k * k);            // J_c J_c^T, then X = its inverse (the exchange ends in this buffer)
+  grow(l.M + r2(margin));
   const int u0 = o;
   l.W = take(nv * 3);           // direction of every dof's motion axis
   l.Pt = take(nv * 3);          // a point on it
   l.pf = take(nc * 3);          // contact points
-  l.Z = u0;                     // Z = X J_c
-  l.M2 = u0;                    // second exchange buffer (W, Pt, pf are dead by then; Z comes after)
-  const int zend = u0 + ((((k * nv > k * k) ? k * nv : k * k) + 1) & ~1);
-  if (o < zend) o = zend;
-  l.Jc = take(k * nv);          // J_c
-  l.M = take(k * k);            // J_c J_c^T, then X = its inverse (the exchange ends in this buffer)
-  l.P = take(nv * nv);          // P = I - J_c^T X J_c
+  l.M2 = u0;                    // second exchange buffer (W, Pt, pf are dead by then)
+  l.Z = u0;                     // Z^T = (X J_c)^T, row r at r * 3 nc (M2 is dead by then)
+  grow(u0 + r2(k * nv > k * k ? k * nv : k * k));
+  if (hw > 0) {
+    l.P = u0 - r2(margin);      // P = I - Z^T J_c
+    grow(l.P + r2(nv * nv));
+  } else {
+    l.P = take(nv * nv);
+  }
+  l.H1 = r2(nv * 6) <= r2(k * nv) ? D : take(nv * 6);  // P[:, ff] J_w[:, ff]^T
   l.total = o;
   return l;
 }
@@ -283,7 +306,8 @@ template <int MAXCH, int NVC, int SPW>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
 #endif
-__global__ void __launch_bounds__(64 * K1_WAVES, SYSID_K1_MIN_WAVES_PER_EU)
+// Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
+__global__ void __launch_bounds__(64 * K1_WAVES, SPW == 2 ? 2 : SYSID_K1_MIN_WAVES_PER_EU)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
                    int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp,
                    unsigned long long* __restrict__ work, double* __restrict__ dbg) {
@@ -318,7 +342,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   static_assert(SPW == 1 || SPW == 2, "1 or 2 samples per wave (4 measured 34% slower)");
   constexpr int HW = 64 / SPW;                       // lanes per sample
   const int half = lane / HW, hl = lane % HW;         // sample slot within the wave, lane within it
-  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc);
+  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0);
   double* wr = smem + kp.mimg_dbl + (wave * SPW + half) * kp.wave_dbl;
   double* body = wr + L.body;
   double* Ws = wr + L.W;
@@ -330,15 +354,28 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   double* Ps = wr + L.P;
   double* H1 = wr + L.H1;
   double* tps = wr + L.tp;
+  double* dqs = wr + L.dqs;
 
   // Samples are handed out SPW at a time from a device counter (work[0]), so a workgroup that becomes
   // resident late, or a slow CU, only ever costs its own last samples.  The next ones are claimed one
   // step ahead and their inputs prefetched into registers (channel c -> lane c, c+HW, ...) while the
   // current ones run.  The last wave to leave resets the counters for the next launch (work[1] counts
   // departed waves; no wave touches work[0] after its last claim returned >= N).
-  auto claim = [&]() -> int64_t {
+  // The prefetch and the claim are issued at the top of a step and consumed in its middle (after the
+  // projector): vmcnt retires in issue order, so consuming them at the top of the next step would first
+  // wait for all of this step's panel stores.
+  auto claim_issue = [&]() -> unsigned long long {
     unsigned long long v = 0;
-    if (lane == 0) v = atomicAdd(work, (unsigned long long)SPW);
+    if (lane == 0) {
+      // an opaque (per-lane) zero offset keeps the atomic optimizer from rewriting the claim as a wave
+      // scan, which reads the returned value (and waits for it) right at the atomic
+      int z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      v = atomicAdd(work + z, (unsigned long long)SPW);
+    }
+    return v;
+  };
+  auto claim_value = [&](unsigned long long v) -> int64_t {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return (int64_t)(((unsigned long long)hi << 32) | lo);
@@ -360,9 +397,18 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const double* tau = ddq + nv;
   const double* cnt = tau + nja;
 
-  int64_t s = claim();
-  int64_t s1 = s < N ? claim() : N;
-  if (s < N) fetch(s);
+  auto commit = [&]() {
+#pragma unroll
+    for (int u = 0; u < NXR; ++u)
+      if (hl + HW * u < IN) sin_[hl + HW * u] = xr[u];
+  };
+
+  int64_t s = claim_value(claim_issue());
+  if (s < N) {
+    fetch(s);
+    commit();
+  }
+  int64_t s1 = s < N ? claim_value(claim_issue()) : N;
 #ifdef SYSID_STAMPS
   unsigned long long t_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
@@ -371,11 +417,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   while (s < N) {
     const bool valid = s + half < N;  // the step's last samples may not exist
     wsync();
-#pragma unroll
-    for (int u = 0; u < NXR; ++u)
-      if (hl + HW * u < IN) sin_[hl + HW * u] = xr[u];
-    const int64_t s2 = s1 < N ? claim() : N;  // used one step from now
     if (s1 < N) fetch(s1);
+    const unsigned long long pend = s1 < N ? claim_issue() : 0ull;  // the step after s1, read mid-step
     for (int x = hl; x < 24; x += HW) {
       double v = 0.0;
       if (x == 0 || x == 4 || x == 8) v = 1.0;   // oR_0 = I
@@ -599,65 +642,69 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       K1_STAMP(4)
 
-      // ---- Z = X J_c ;  P = I - J_c^T Z ----
-      double* Zs = wr + L.Z;
+      // ---- Z = X J_c (stored transposed) ;  P = I - Z^T J_c ----
+      // P's entries are produced row-major, HW per pass, and a pass may overwrite Z rows that earlier
+      // passes consumed (wave_layout); the ordering point after each pass keeps the passes in order.
+      double* Zt = wr + L.Z;
+      const int K = 3 * nc;
       for (int e = hl; e < k * nv; e += HW) {
-        const int a = e / nv, r = e - a * nv;
+        const int r = e / k, a = e - r * k;
         double acc = 0.0;
 #pragma unroll 4
         for (int b = 0; b < k; ++b) acc += Xs[a * k + b] * Jc[b * nv + r];
-        Zs[e] = acc;
+        Zt[r * K + a] = acc;
       }
       wsync();
       for (int e = hl; e < nv * nv; e += HW) {
         const int a = e / nv, b = e - a * nv;
+        const double* za = Zt + a * K;
         double acc = 0.0;
 #pragma unroll 4
-        for (int j = 0; j < k; ++j) acc += Jc[j * nv + a] * Zs[j * nv + b];
+        for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
         Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+        wsync();
       }
-      wsync();
     }
     K1_STAMP(5)
 
-    // ---- H1 = P[:, ff] J_w[:, ff]^T ;  tp = P S^T tau ----
-    for (int e = hl; e < nv * 7; e += HW) {
-      if (e < nv * 6) {
-        const int r = e / 6, c = e - 6 * r;
-        double h = 0.0;
-        if (kp.has_ff)
-          for (int d = 0; d < 6; ++d) h += Ps[r * nv + kp.ff0 + d] * Jws[6 * (kp.ff0 + d) + c];
-        H1[e] = h;
-      } else {
-        const int r = e - nv * 6;
-        double acc = 0.0;
+    // ---- tp = P S^T tau  (+ J_c^T lambda in the full mode) ;  H1 = P[:, ff] J_w[:, ff]^T ----
+    // tp first: in the full mode H1 may be stored over J_c (overlay layout), which the tau column reads.
+    for (int r = hl; r < nv; r += HW) {
+      double acc = 0.0;
 #pragma unroll 4
-        for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
-        if (kp.full) {
-          // + J_c^T lambda, lambda = the measured forces of the feet in contact in foot order, world axes
-          // (LOCAL_WORLD_ALIGNED).  J_c here is in base axes, J_c,world = R_b J_c, so lambda is moved to
-          // base axes with R_b^T (R_b = the base quaternion's matrix, unnormalised like pinocchio's).
-          double Rb[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-          if (kp.has_ff && jtype[1] == JT_FREEFLYER) {
-            const int iq = idx_q[1];
-            quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], Rb);
-          }
-          const double* lam = cnt + nc;
-          for (int rho = 0, c = -1; rho < k; ++rho) {
-            const int comp = rho % 3;
-            if (comp == 0)
-              for (++c; c < nc && cnt[c] == 0.0; ++c) {}
-            const double* lw = lam + 3 * c;
-            // column `comp` of R_b by selects (a dynamic index would put Rb in scratch memory)
-            const double c0 = comp == 0 ? Rb[0] : (comp == 1 ? Rb[1] : Rb[2]);
-            const double c1 = comp == 0 ? Rb[3] : (comp == 1 ? Rb[4] : Rb[5]);
-            const double c2 = comp == 0 ? Rb[6] : (comp == 1 ? Rb[7] : Rb[8]);
-            const double lb = c0 * lw[0] + c1 * lw[1] + c2 * lw[2];
-            acc += Jc[rho * nv + r] * lb;
-          }
+      for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
+      if (kp.full) {
+        // + J_c^T lambda, lambda = the measured forces of the feet in contact in foot order, world axes
+        // (LOCAL_WORLD_ALIGNED).  J_c here is in base axes, J_c,world = R_b J_c, so lambda is moved to
+        // base axes with R_b^T (R_b = the base quaternion's matrix, unnormalised like pinocchio's).
+        double Rb[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        if (kp.has_ff && jtype[1] == JT_FREEFLYER) {
+          const int iq = idx_q[1];
+          quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], Rb);
         }
-        tps[r] = acc;
+        const double* lam = cnt + nc;
+        for (int rho = 0, c = -1; rho < k; ++rho) {
+          const int comp = rho % 3;
+          if (comp == 0)
+            for (++c; c < nc && cnt[c] == 0.0; ++c) {}
+          const double* lw = lam + 3 * c;
+          // column `comp` of R_b by selects (a dynamic index would put Rb in scratch memory)
+          const double c0 = comp == 0 ? Rb[0] : (comp == 1 ? Rb[1] : Rb[2]);
+          const double c1 = comp == 0 ? Rb[3] : (comp == 1 ? Rb[4] : Rb[5]);
+          const double c2 = comp == 0 ? Rb[6] : (comp == 1 ? Rb[7] : Rb[8]);
+          const double lb = c0 * lw[0] + c1 * lw[1] + c2 * lw[2];
+          acc += Jc[rho * nv + r] * lb;
+        }
       }
+      tps[r] = acc;
+    }
+    if (kp.full) wsync();
+    for (int e = hl; e < nv * 6; e += HW) {
+      const int r = e / 6, c = e - 6 * r;
+      double h = 0.0;
+      if (kp.has_ff)
+        for (int d = 0; d < 6; ++d) h += Ps[r * nv + kp.ff0 + d] * Jws[6 * (kp.ff0 + d) + c];
+      H1[e] = h;
     }
     wsync();
     if (dbg != nullptr && s + half == 0) {
@@ -665,6 +712,14 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       for (int x = hl; x < L.total; x += HW) dbg[x] = wr[x];  // diagnostics: LDS image of sample 0
 #endif
     }
+    // mid-step: the next inputs go to `in` (the friction columns keep this sample's dq in dqs)
+    for (int x = hl; x < nv; x += HW) dqs[x] = dq[x];
+    unsigned long long pv = pend;
+    asm volatile("" : "+v"(pv));  // keeps the read of the claim (and its vmcnt wait) here
+    const int64_t s2 = s1 < N ? claim_value(pv) : N;
+    wsync();
+    if (s1 < N) commit();
+    wsync();
     K1_STAMP(6)
 
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
@@ -726,7 +781,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const bool coul = jj >= nja;
           const int j = coul ? jj - nja : jj;
           const int jc = j < nja ? j : nja - 1;          // clamp for the tau/pad columns
-          const double x = dq[bd + jc];
+          const double x = dqs[bd + jc];
           const double sc = coul ? sign_of(x) : x;
           const double fr = pr[jc] * sc;
           v2[u] = jj < 2 * nja ? fr : (kp.wy + jj == kp.w ? tps[r] : 0.0);  // pad: keep lines whole

@@ -38,7 +38,7 @@ def world_axes(model, d):
 
 def projector_exchange(model, d, cnt, W, Pt, lin, thr_rel=1e-13):
     """P = I - J_c^T X J_c with X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, pivots <= thr_rel * max diag
-    dropped (their row and column of X zeroed), as K1 computes it."""
+    dropped (their row and column of X zeroed), as K1 computes it: Z = X J_c, P = I - Z^T J_c."""
     rows = []
     for k, f in enumerate(model.contact_frames()):
         if not cnt[k]:
@@ -64,7 +64,7 @@ def projector_exchange(model, d, cnt, W, Pt, lin, thr_rel=1e-13):
         Y[j, j] = ip
         X = Y
     Z = X @ Jc
-    return np.eye(nv) - Jc.T @ Z
+    return np.eye(nv) - Z.T @ Jc
 
 
 def base_relative(model, d):
