@@ -228,12 +228,8 @@ __device__ __forceinline__ void panel_store(double2* p, double2 v) { *p = v; }
 #define K1_STAMP(k)
 #endif
 
-// All ten columns of pinocchio's bodyRegressor for body i, moved to the free-flyer frame, in a compact
-// layout: columns 0..3 (m, mc) as [linear(3); angular(3)] in F[0..23]; columns 4..9 (inertia) have a
-// zero force part, only their angular rows are kept in F[24..41].  bi = {oR(9), ot(3), v(6), a_gf(6)}.
-constexpr int FBLK = 42;
-
-__host__ __device__ inline void body_regressor_block(const double* bi, double* F) {
+// Columns 0..3 (m, mc) of the block: F[6c .. 6c+5] = [linear; angular] of column c.
+__host__ __device__ inline void body_block_mass(const double* bi, double* F) {
   const double* R = bi;
   const double* t = bi + 9;
   const double* v = bi + 12;
@@ -267,7 +263,13 @@ __host__ __device__ inline void body_regressor_block(const double* bi, double* F
     c[0] = Rf[0]; c[1] = Rf[1]; c[2] = Rf[2];
     c[3] = Rn[0] + tf[0]; c[4] = Rn[1] + tf[1]; c[5] = Rn[2] + tf[2];
   }
-  // columns 4..9 (Ixx, Ixy, Iyy, Ixz, Iyz, Izz): f = 0, n = I dw + w x (I w)
+}
+
+// Columns 4..9 (Ixx, Ixy, Iyy, Ixz, Iyz, Izz): f = 0, n = I dw + w x (I w); F[3q .. 3q+2] = angular part.
+__host__ __device__ inline void body_block_inertia(const double* bi, double* F) {
+  const double* R = bi;
+  const double* w = bi + 15;
+  const double* dw = bi + 21;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
     const double s0 = q == 0, s1 = q == 1, s2 = q == 2, s3 = q == 3, s4 = q == 4, s5 = q == 5;
@@ -280,8 +282,18 @@ __host__ __device__ inline void body_regressor_block(const double* bi, double* F
     bw[2] = s3 * w[0] + s4 * w[1] + s5 * w[2];
     cross3(w, bw, x);
     n[0] = bdw[0] + x[0]; n[1] = bdw[1] + x[1]; n[2] = bdw[2] + x[2];
-    mat3vec(R, n, F + 24 + 3 * q);
+    mat3vec(R, n, F + 3 * q);
   }
+}
+
+// All ten columns of pinocchio's bodyRegressor for body i, moved to the free-flyer frame, in a compact
+// layout: columns 0..3 (m, mc) as [linear(3); angular(3)] in F[0..23]; columns 4..9 (inertia) have a
+// zero force part, only their angular rows are kept in F[24..41].  bi = {oR(9), ot(3), v(6), a_gf(6)}.
+constexpr int FBLK = 42;
+
+__host__ __device__ inline void body_regressor_block(const double* bi, double* F) {
+  body_block_mass(bi, F);
+  body_block_inertia(bi, F + 24);
 }
 
 // Column p of the block as a 6-vector [linear; angular] (diagnostics and tests).
@@ -340,6 +352,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const int nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   static_assert(SPW == 1 || SPW == 2, "1 or 2 samples per wave (4 measured 34% slower)");
+  constexpr bool OPQ = NVC == 18;  // quadruped variant: see the top of the sample loop
   constexpr int HW = 64 / SPW;                       // lanes per sample
   const int half = lane / HW, hl = lane % HW;         // sample slot within the wave, lane within it
   const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0);
@@ -414,7 +427,35 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
+  const int hl_outer = hl;
   while (s < N) {
+    // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
+    // step, so the per-lane index arithmetic of the phase loops (nv is a compile-time constant) and the
+    // pointers into the region are recomputed per step instead of being hoisted out of the sample loop
+    // into hundreds of live registers (Spot K1 -3%).  Elsewhere these are plain loop invariants.
+    int hl = hl_outer;
+    int woff = (wave * SPW + half) * kp.wave_dbl;
+    if constexpr (OPQ) {
+      asm volatile("" : "+v"(hl));
+      asm volatile("" : "+v"(woff));
+    }
+    double* wr = smem + kp.mimg_dbl + woff;
+    double* body = wr + L.body;
+    double* Ws = wr + L.W;
+    double* Pts = wr + L.Pt;
+    double* Jws = wr + L.Jw;
+    double* pfs = wr + L.pf;
+    double* Jc = wr + L.Jc;
+    double* Ms = wr + L.M;
+    double* Ps = wr + L.P;
+    double* H1 = wr + L.H1;
+    double* tps = wr + L.tp;
+    double* dqs = wr + L.dqs;
+    const double* q = wr + L.in;
+    const double* dq = q + nq;
+    const double* ddq = dq + nv;
+    const double* tau = ddq + nv;
+    const double* cnt = tau + nja;
     const bool valid = s + half < N;  // the step's last samples may not exist
     wsync();
     if (s1 < N) fetch(s1);
@@ -745,13 +786,25 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         double G[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) G[k] = h[k];
+        if constexpr (OPQ) {
+          // unconditional loads (dof[t] = 0 past the chain is a valid slot), masked products
 #pragma unroll
-        for (int t = 0; t < MAXCH; ++t) {
-          if (t < cl) {
-            const double pv = pr[dof[t]];
+          for (int t = 0; t < MAXCH; ++t) {
+            const double pl = pr[dof[t]];
+            const double pv = t < cl ? pl : 0.0;
             const double* jw = Jws + 6 * dof[t];
 #pragma unroll
             for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < MAXCH; ++t) {
+            if (t < cl) {
+              const double pv = pr[dof[t]];
+              const double* jw = Jws + 6 * dof[t];
+#pragma unroll
+              for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
+            }
           }
         }
         double y[10];
