@@ -429,7 +429,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.in_lds = in_lds; kp.full = 0;
   kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL.total; kp.out_cols = e->ldp;
   kp.rg = k1_row_groups(NJ, 64);  // per launch: k1_row_groups(NJ, lanes per sample)
-  kp.thr_rel = 1e-13;
+  kp.thr_rel = 1e-14;  // rank cut of the Gram-Schmidt projector (pinv: 1e-15 sigma_max)
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
   e->k1_maxch_tpl = maxch_tpl;
 

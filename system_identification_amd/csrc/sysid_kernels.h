@@ -68,7 +68,7 @@ __host__ __device__ inline int k1_row_groups(int NJ, int lanes) {
 constexpr int BODY_STRIDE = 26;
 
 // Per-wave LDS region of K1 (doubles, every piece 16-B aligned).  The projector's working set
-// D = [J_c | M | W,Pt,pf / M2 / Z] is dead once P is built, and holds its results too:
+// D = [J_c | M | W,Pt,pf / Z] is dead once P is built, and holds its results too:
 //   * H1 over J_c (stored after the tau column, which reads J_c in the full mode), or after everything
 //     when J_c's slot is smaller;
 //   * with `hw` > 0 (lanes per sample of a compile-time-nv kernel) P ends inside Z's slot: P is built
@@ -78,7 +78,7 @@ constexpr int BODY_STRIDE = 26;
 //     Spot: 1,582 -> 1,158 doubles per sample, so 8 two-sample waves share a CU's 160 KB (was 6).
 //   * otherwise P follows D.
 struct WLay {
-  int in, body, W, Pt, Jw, pf, Jc, M, M2, P, H1, tp, dqs, Z, total;
+  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, dqs, Z, total;
 };
 
 __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc, int hw) {
@@ -101,17 +101,17 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc,
       const int lead = E - k * (E / nv);
       if (lead > margin) margin = lead;
     }
-  l.M = take(k * k);            // J_c J_c^T, then X = its inverse (the exchange ends in this buffer)
+  l.M = take(k * k);            // row norms of the Gram-Schmidt pass (k used)
   grow(l.M + r2(margin));
   const int u0 = o;
   l.W = take(nv * 3);           // direction of every dof's motion axis
   l.Pt = take(nv * 3);          // a point on it
   l.pf = take(nc * 3);          // contact points
-  l.M2 = u0;                    // second exchange buffer (W, Pt, pf are dead by then)
-  l.Z = u0;                     // Z^T = (X J_c)^T, row r at r * 3 nc (M2 is dead by then)
+  l.Z = u0;                     // Q^T (orthonormal rows of J_c's row space), row r at r * 3 nc (W, Pt, pf
+                                // are dead by then)
   grow(u0 + r2(k * nv > k * k ? k * nv : k * k));
   if (hw > 0) {
-    l.P = u0 - r2(margin);      // P = I - Z^T J_c
+    l.P = u0 - r2(margin);      // P = I - Q^T Q
     grow(l.P + r2(nv * nv));
   } else {
     l.P = take(nv * nv);
@@ -127,7 +127,7 @@ struct K1Params {
   int in_lds;       // input channels the LDS layout holds (in_rows of the full-force mode)
   int full;         // 1: get_full_regressor_force mode (P = I, tau column = S^T tau + J_c^T lambda)
   int rg;           // row groups of the regressor-column phase (lanes = bodies x rg)
-  double thr_rel;   // pivot cut of the J_c J_c^T inversion (relative to its max diagonal)
+  double thr_rel;   // rank cut of the projector: remaining row norm <= thr_rel * the largest row norm
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
 };
 
@@ -210,6 +210,107 @@ __device__ inline double sign_of(double x) {
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+}
+
+// 1/sqrt(x) for x > 0: the hardware estimate refined by two Newton steps (~1 ulp; no division).
+__device__ __forceinline__ double rsqrt_f64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  y = y * (1.5 - h * y * y);
+  y = y * (1.5 - h * y * y);
+  return y;
+}
+
+// v + v of another lane, by a DPP lane pattern on both halves of the double (the partner lane must be
+// active: callers keep whole lane groups together).
+template <int CTRL>
+__device__ __forceinline__ double dpp_add(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return v + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double pair_sum(double v) { return dpp_add<0xB1>(v); }  // quad_perm [1,0,3,2]
+
+// Sum over an aligned group of `lpr` lanes (1, 2, 4 or 8; uniform over the group): lane ^ 1, lane ^ 2,
+// then the half-row mirror (lane i <-> 7 - i pairs the two quads of an 8-lane group).
+__device__ __forceinline__ double group_sum(double v, int lpr) {
+  if (lpr >= 2) v = dpp_add<0xB1>(v);
+  if (lpr >= 4) v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (lpr >= 8) v = dpp_add<0x141>(v);  // row_half_mirror
+  return v;
+}
+
+// |x|^2 of a row of nv doubles (three partial sums).
+template <int NVC>
+__device__ __forceinline__ double mgs_sqnorm(const double* x, int nv_rt) {
+  const int nv = NVC > 0 ? NVC : nv_rt;
+  double a[3] = {0.0, 0.0, 0.0};
+#pragma unroll 6
+  for (int r = 0; r < nv; ++r) a[r % 3] += x[r] * x[r];
+  return (a[0] + a[1]) + a[2];
+}
+
+// One Gram-Schmidt step on a row x still in play, against the pivot row xp (q = xp / |xp|, inv2 =
+// 1 / |xp|^2): x -= ((xp . x) inv2) xp = (q . x) q.  Returns x's new squared norm (recomputed, not
+// downdated: the rank cut needs the small ones accurate).  The pivot row itself is not touched (its
+// lane skips the step), so no load of xp can see a store of the pass.
+// Runtime nv: a group of lpr lanes per row, lane h of the group taking entries h, h + lpr, ...; the dot
+// product and the norm are completed across the group.  All lanes of the group return the new norm.
+__device__ __forceinline__ double mgs_step_group(const double* xp, double* x, double inv2, int nv, int h, int lpr) {
+  double c0 = 0.0, c1 = 0.0;
+  for (int r = h; r < nv; r += 2 * lpr) {
+    c0 += xp[r] * x[r];
+    if (r + lpr < nv) c1 += xp[r + lpr] * x[r + lpr];
+  }
+  const double c = group_sum(c0 + c1, lpr) * inv2;
+  double a0 = 0.0, a1 = 0.0;
+  for (int r = h; r < nv; r += 2 * lpr) {
+    const double v0 = x[r] - c * xp[r];
+    x[r] = v0;
+    a0 += v0 * v0;
+    if (r + lpr < nv) {
+      const double v1 = x[r + lpr] - c * xp[r + lpr];
+      x[r + lpr] = v1;
+      a1 += v1 * v1;
+    }
+  }
+  return group_sum(a0 + a1, lpr);
+}
+
+// Compile-time nv = NVC: two lanes per row (lane pair 2j, 2j+1 takes entries [0, H) and [H, NVC) of
+// row j, H = NVC/2 rounded up to even so both halves start 16-byte aligned); the dot product and the norm
+// are completed across the pair with DPP.  Both lanes of a pair return the row's new squared norm.
+template <int NVC>
+__device__ __forceinline__ double mgs_step_pair(const double* xp, double* x, double inv2, int h) {
+  constexpr int H = ((NVC + 1) / 2 + 1) & ~1;
+  constexpr int H2 = H / 2;
+  const double2* xp2 = reinterpret_cast<const double2*>(xp + h * H);
+  double2* x2 = reinterpret_cast<double2*>(x + h * H);
+  const int n2 = h == 0 ? H2 : (NVC - H) / 2;  // double2 entries of this lane's half (NVC even)
+  double2 pv[H2], xv[H2];
+#pragma unroll
+  for (int u = 0; u < H2; ++u) {
+    pv[u] = u < n2 ? xp2[u] : make_double2(0.0, 0.0);
+    xv[u] = u < n2 ? x2[u] : make_double2(0.0, 0.0);
+  }
+  double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+  for (int u = 0; u < H2; ++u) {
+    c0 += pv[u].x * xv[u].x;
+    c1 += pv[u].y * xv[u].y;
+  }
+  const double c = pair_sum(c0 + c1) * inv2;
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int u = 0; u < H2; ++u) {
+    xv[u].x -= c * pv[u].x;
+    xv[u].y -= c * pv[u].y;
+    a0 += xv[u].x * xv[u].x;
+    a1 += xv[u].y * xv[u].y;
+    if (u < n2) x2[u] = xv[u];
+  }
+  return pair_sum(a0 + a1);
 }
 
 // Panel stores (plain: non-temporal stores measured equal on Spot and 2.5x slower K1 on G1).
@@ -312,7 +413,7 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 // MAXCH: chain-slot count (>= longest revolute chain).  NVC: nv fixed at compile time (0 = read it
 // from K1Params), so the row loops of the common robots unroll with immediate LDS offsets.
 // SPW: samples per wave (1 or 2).  With SPW > 1 each 64/SPW-lane slice of the wave carries its own
-// sample through every phase, so the lane-starved serial phases (forward pass, exchange steps) do SPW
+// sample through every phase, so the lane-starved serial phases (forward pass, Gram-Schmidt steps) do SPW
 // samples per instruction; each slice has its own LDS region.
 template <int MAXCH, int NVC, int SPW>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
@@ -352,7 +453,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const int nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   static_assert(SPW == 1 || SPW == 2, "1 or 2 samples per wave (4 measured 34% slower)");
-  constexpr bool OPQ = NVC == 18;  // quadruped variant: see the top of the sample loop
+  constexpr bool OPQ = true;               // opaque per-sample lane index / LDS pointers (top of the loop)
+  constexpr bool CHAIN_UNCOND = NVC == 18;  // unconditional chain loads in the column phase
   constexpr int HW = 64 / SPW;                       // lanes per sample
   const int half = lane / HW, hl = lane % HW;         // sample slot within the wave, lane within it
   const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0);
@@ -625,77 +727,90 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       wsync();
     } else {
-      // ---- M = J_c J_c^T, into the exchange buffer that makes the k ping-pong steps end in Ms ----
-      double* M0 = (k & 1) ? wr + L.M2 : Ms;
-      for (int e = hl; e < k * k; e += HW) {
-        const int a = e / k, b = e - a * k;
-        double acc = 0.0;
-#pragma unroll 6
-        for (int r = 0; r < nv; ++r) acc += Jc[a * nv + r] * Jc[b * nv + r];
-        M0[e] = acc;
-      }
+      // ---- orthonormal basis of J_c's row space by pivoted modified Gram-Schmidt ----
+      // P = I - pinv(J_c) J_c is the projector onto null(J_c) = I - Q^T Q for any orthonormal basis Q of
+      // the row space.  Step t takes the row with the largest remaining norm (first on ties) as
+      // q = x_p / |x_p| and removes its direction from every row still in play (lane = row slot, one
+      // wave-synchronous pass per step).  Rows whose remaining norm is <= thr_rel * the largest row norm
+      // are dependent on the taken ones and dropped, as pinv drops singular values <= 1e-15 sigma_max.
+      // The error is ~eps * cond(J_c), pinv's own order (the normal-equations inverse it replaces was
+      // eps * cond^2: 1e-5 at cond 1e6).  q of slot j ends in J_c row j (in place) and, transposed, in
+      // column j of Zt (stride 3 nc); dropped slots are zero in Zt, so P below sums over all k slots.
+      double* nrm = Ms;  // squared remaining norm of each row slot, -1 once taken
+      double* Zt = wr + L.Z;
+      const int K = 3 * nc;
+      for (int j = hl; j < k; j += HW) nrm[j] = mgs_sqnorm<NVC>(Jc + j * nv, nv);
       wsync();
       K1_STAMP(3)
-
-      // ---- X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, ping-ponging between two LDS buffers ----
-      // One pivot per step (no square roots, one reciprocal); every entry of a step reads only the
-      // previous buffer, so each step is a single wave-synchronous pass.  A pivot <= thr_rel * max diag
-      // (a contact row dependent on the kept ones) is dropped: ip = 0 zeroes its row and column and
-      // leaves the rest untouched, i.e. X is the inverse on the kept rows, as pinv treats them.
-      const double* Xs = Ms;
       {
-        double dmax = 0.0;
-        for (int a = 0; a < k; ++a) dmax = fmax(dmax, M0[a * k + a]);
-        const double thr = kp.thr_rel * dmax;
-        const float rk = k > 0 ? 1.0f / (float)k : 0.0f;
-        double* src = M0;
-        double* dst = (k & 1) ? Ms : wr + L.M2;
-        for (int j = 0; j < k; ++j) {
-          const double pj = src[j * k + j];
-          // three entries per lane per pass: all their loads issue before any store of the pass
-          for (int e0 = hl; e0 < k * k; e0 += 3 * HW) {
-            int r[3], c[3];
-            double arc[3], arj[3], ajc[3];
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-              const int e = e0 + HW * u;
-              const int ee = e < k * k ? e : 0;
-              r[u] = (int)(((float)ee + 0.5f) * rk);  // exact: ee < 24*24
-              c[u] = ee - r[u] * k;
-              arc[u] = src[ee];
-              arj[u] = src[r[u] * k + j];
-              ajc[u] = src[j * k + c[u]];
+        double nmax = 0.0;
+        for (int j = 0; j < k; ++j) nmax = fmax(nmax, nrm[j]);
+        const double thr = kp.thr_rel * kp.thr_rel * nmax;
+        // lane pairs per row for the compile-time-nv kernel when the rows fit (uniform per sample)
+        const bool pairs = NVC > 0 && NVC % 2 == 0 && 2 * k <= HW;
+        // otherwise lane groups of lpr = 8, 4, 2 or 1 lanes per row, the widest whose rows fit
+        const int lpr = 8 * k <= HW ? 8 : (4 * k <= HW ? 4 : (2 * k <= HW ? 2 : 1));
+        for (int t = 0; t < k; ++t) {
+          int p = 0;
+          double best = -1.0;
+          for (int j = 0; j < k; ++j) {
+            const double v = nrm[j];
+            if (v > best) { best = v; p = j; }
+          }
+          if (!(best > thr)) break;  // uniform within the sample's lanes
+          const double inv = rsqrt_f64(best);
+          const double inv2 = inv * inv;
+          const double* xp = Jc + p * nv;
+          if constexpr (NVC > 0 && NVC % 2 == 0) {
+            if (pairs) {
+              const int j = hl >> 1;
+              // taken slots keep their scale as -1/|x_p| (the pivot's row is final: scaled below)
+              const double nj = j < k ? nrm[j] : -1.0;
+              if (j == p) {
+                if ((hl & 1) == 0) nrm[p] = -inv;
+              } else if (nj >= 0.0) {
+                const double a = mgs_step_pair<NVC>(xp, Jc + j * NVC, inv2, hl & 1);
+                if ((hl & 1) == 0) nrm[j] = a;
+              }
             }
-            const double ip = pj > thr ? 1.0 / pj : 0.0;
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-              const double v = r[u] == j ? (c[u] == j ? ip : ajc[u] * ip)
-                                         : (c[u] == j ? -arj[u] * ip : arc[u] - arj[u] * ajc[u] * ip);
-              if (e0 + HW * u < k * k) dst[e0 + HW * u] = v;
+          }
+          if (!pairs) {
+            if (k * lpr <= HW) {
+              const int j = hl / lpr, h = hl - j * lpr;
+              const double nj = j < k ? nrm[j] : -1.0;
+              if (j == p) {
+                if (h == 0) nrm[p] = -inv;
+              } else if (nj >= 0.0) {
+                const double a = mgs_step_group(xp, Jc + j * nv, inv2, nv, h, lpr);
+                if (h == 0) nrm[j] = a;
+              }
+            } else {
+              for (int j = hl; j < k; j += HW) {
+                if (j == p) {
+                  nrm[p] = -inv;
+                } else if (nrm[j] >= 0.0) {
+                  nrm[j] = mgs_step_group(xp, Jc + j * nv, inv2, nv, 0, 1);
+                }
+              }
             }
           }
           wsync();
-          double* t = src;
-          src = dst;
-          dst = t;
         }
-        Xs = src;  // == Ms: Z below overwrites the shared region that held the other buffer
+        // q of each taken slot = its row x 1/|x_p| (in place, and transposed into Zt); dropped slots: 0
+        for (int e = hl; e < k * nv; e += HW) {
+          const int j = e / nv, r = e - j * nv;
+          const double sc = nrm[j] < 0.0 ? -nrm[j] : 0.0;
+          const double qv = Jc[e] * sc;
+          Jc[e] = qv;
+          Zt[r * K + j] = qv;
+        }
+        wsync();
       }
       K1_STAMP(4)
 
-      // ---- Z = X J_c (stored transposed) ;  P = I - Z^T J_c ----
-      // P's entries are produced row-major, HW per pass, and a pass may overwrite Z rows that earlier
+      // ---- P = I - Q^T Q  (Zt row a = column a of Q; J_c rows = rows of Q) ----
+      // P's entries are produced row-major, HW per pass, and a pass may overwrite Zt rows that earlier
       // passes consumed (wave_layout); the ordering point after each pass keeps the passes in order.
-      double* Zt = wr + L.Z;
-      const int K = 3 * nc;
-      for (int e = hl; e < k * nv; e += HW) {
-        const int r = e / k, a = e - r * k;
-        double acc = 0.0;
-#pragma unroll 4
-        for (int b = 0; b < k; ++b) acc += Xs[a * k + b] * Jc[b * nv + r];
-        Zt[r * K + a] = acc;
-      }
-      wsync();
       for (int e = hl; e < nv * nv; e += HW) {
         const int a = e / nv, b = e - a * nv;
         const double* za = Zt + a * K;
@@ -786,7 +901,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         double G[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) G[k] = h[k];
-        if constexpr (OPQ) {
+        if constexpr (CHAIN_UNCOND) {
           // unconditional loads (dof[t] = 0 past the chain is a valid slot), masked products
 #pragma unroll
           for (int t = 0; t < MAXCH; ++t) {

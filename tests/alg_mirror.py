@@ -3,7 +3,8 @@
 The kernel does not follow pinocchio's backward pass.  It uses, per sample:
 
 * motion axes of every dof in the base (free-flyer) frame: ``w_r`` (direction) and ``p_r`` (a point);
-* the contact Jacobian from the same axes; ``P = I - Q^T Q`` with ``Q = L^-1 J_c``, ``L L^T = J_c J_c^T``;
+* the contact Jacobian from the same axes; ``P = I - Q^T Q`` with the rows of ``Q`` an orthonormal basis of
+  J_c's row space (pivoted modified Gram-Schmidt);
 * ``H_i = P · M_i · J_w^T`` (nv x 6, world coordinates), built by one rank-1 update per body from its
   parent (``M_i`` = mask of the dofs supporting body i);
 * each regressor column of body i as ``H_i · f^w`` with ``f^w`` the body-regressor column moved to world.
@@ -36,9 +37,7 @@ def world_axes(model, d):
     return W, Pt, lin
 
 
-def projector_exchange(model, d, cnt, W, Pt, lin, thr_rel=1e-13):
-    """P = I - J_c^T X J_c with X = (J_c J_c^T)^-1 by Gauss-Jordan exchange, pivots <= thr_rel * max diag
-    dropped (their row and column of X zeroed), as K1 computes it: Z = X J_c, P = I - Z^T J_c."""
+def contact_jacobian(model, d, cnt, W, Pt, lin):
     rows = []
     for k, f in enumerate(model.contact_frames()):
         if not cnt[k]:
@@ -48,23 +47,32 @@ def projector_exchange(model, d, cnt, W, Pt, lin, thr_rel=1e-13):
         for r in model.support_dofs(f.parent):
             J[:, r] = W[r] if lin[r] else np.cross(W[r], pf - Pt[r])
         rows.append(J)
-    nv = model.nv
-    if not rows:
-        return np.eye(nv)
-    Jc = np.vstack(rows)
-    X = Jc @ Jc.T
-    k = X.shape[0]
-    thr = thr_rel * np.max(np.diag(X))
-    for j in range(k):
-        p = X[j, j]
-        ip = 1.0 / p if p > thr else 0.0
-        Y = X - np.outer(X[:, j], X[j, :]) * ip
-        Y[j, :] = X[j, :] * ip
-        Y[:, j] = -X[:, j] * ip
-        Y[j, j] = ip
-        X = Y
-    Z = X @ Jc
-    return np.eye(nv) - Z.T @ Jc
+    return np.vstack(rows) if rows else np.zeros((0, model.nv))
+
+
+def projector_mgs(Jc, thr_rel=1e-14):
+    """P = I - Q^T Q with the rows of Q an orthonormal basis of J_c's row space by pivoted modified
+    Gram-Schmidt, as K1 computes it: step t takes the row with the largest remaining norm (first on ties),
+    rows whose remaining norm is <= thr_rel * the largest row norm are dropped (pinv's rank cut)."""
+    X = np.array(Jc, dtype=np.float64)
+    k, nv = X.shape
+    nrm = np.einsum("ij,ij->i", X, X)
+    thr = thr_rel * thr_rel * (nrm.max() if k else 0.0)
+    scale = np.zeros(k)  # 1/|x_p| of each taken slot; 0 for dropped slots
+    for _ in range(k):
+        p = int(np.argmax(nrm))
+        best = nrm[p]
+        if not best > thr:
+            break
+        inv = 1.0 / np.sqrt(best)
+        scale[p] = inv
+        nrm[p] = -1.0
+        for j in range(k):
+            if nrm[j] >= 0.0:
+                X[j] = X[j] - ((X[p] @ X[j]) * (inv * inv)) * X[p]
+                nrm[j] = X[j] @ X[j]
+    Q = X * scale[:, None]
+    return np.eye(nv) - Q.T @ Q
 
 
 def base_relative(model, d):
@@ -83,7 +91,7 @@ def sample_panel(model, q, dq, ddq, tau, cnt):
     """[Y_proj | B_v | B_c | tau_proj] for one sample via the kernel formulation."""
     d = base_relative(model, ref.forward_pass(model, q, dq, ddq))
     W, Pt, lin = world_axes(model, d)
-    P = projector_exchange(model, d, cnt, W, Pt, lin)
+    P = projector_mgs(contact_jacobian(model, d, cnt, W, Pt, lin))
     nv, nb = model.nv, model.nb
     Jw = np.zeros((6, nv))  # world spatial axes [linear at origin; angular]
     for r in range(nv):

@@ -44,7 +44,7 @@ def test_c_oracle_matches_golden(robot):
 
 @pytest.mark.parametrize("robot", ROBOTS)
 def test_kernel_formulation_matches_golden(robot):
-    """The HIP kernel's algebra (world axes, exchange-inverse projector, H1 + revolute chain) in numpy."""
+    """The HIP kernel's algebra (world axes, Gram-Schmidt projector, H1 + revolute chain) in numpy."""
     g, m = load(robot), load_robot(robot)
     nv = m.nv
     scales = unprojected_scales(m, g["q"], g["dq"], g["ddq"], g["tau"])
@@ -52,7 +52,7 @@ def test_kernel_formulation_matches_golden(robot):
         Y, t, Bv, Bc = am.sample_panel(m, g["q"][:, s], g["dq"][:, s], g["ddq"][:, s], g["tau"][:, s], g["contact"][:, s])
         sl = slice(s * nv, (s + 1) * nv)
         for a, b, c in zip((Y, t, Bv, Bc), (g["Y_proj"][sl], g["tau_proj"][sl], g["B_v"][sl], g["B_c"][sl]), scales[s]):
-            # north_star parity bar; (J_c J_c^T)^-1 projector error ~ eps·cond(J_c)^2 (floor: tests/parity.py)
+            # north_star parity bar; Gram-Schmidt projector error ~ eps·cond(J_c), pinv-grade (floor: tests/parity.py)
             assert rel_floor(a, b, c) < 1e-6
 
 

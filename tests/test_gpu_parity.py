@@ -89,6 +89,39 @@ def test_degenerate_inputs():
     assert empty["Y_proj"].shape == (0, 130) and not empty["gram"].any() and empty["btb"] == 0.0
 
 
+def test_ill_conditioned_contact_jacobians():
+    """solo12_fixed standing on nearly straight legs: cond(J_c) ~5/eps up to 5e8, and exactly singular legs
+    (eps = 0, pinv drops 4 directions).  The Gram-Schmidt projector stays pinv-grade (tests/test_projector.py)."""
+    model = load_robot("solo12_fixed")
+    knees = [i for i, n in enumerate(model.joint_names) if n.endswith("KFE")]
+    eps = [1e-2, 1e-4, 1e-6, 1e-8, 0.0]
+    pats = [[1, 1, 1, 0], [1, 0, 2, 0], [1, 1, 1, 1], [0, 1, 1, 1]]
+    n = len(eps) * len(pats)
+    d = generate(model, n, config_index=3)
+    cnt = np.zeros((4, n))
+    for s in range(n):
+        for j in knees:
+            d["q"][model.idx_q[j], s] = eps[s % len(eps)]
+        cnt[:, s] = pats[s // len(eps)]
+    out = eng("solo12_fixed").build(d["q"], d["dq"], d["ddq"], d["tau"], cnt, EMIT_ALL)
+    Y, t = ref.get_projected_y_tau(model, d["q"], d["dq"], d["ddq"], d["tau"], cnt)
+    Bv, Bc = ref.get_projected_friction_regressors(model, d["q"], d["dq"], d["ddq"], cnt)
+    nv = model.nv
+    scales = unprojected_scales(model, d["q"], d["dq"], d["ddq"], d["tau"])
+    for s in range(n):
+        sl = slice(s * nv, (s + 1) * nv)
+        pinned = cnt[:, s].all() and eps[s % len(eps)] != 0.0  # J_c square, invertible: P = 0 exactly
+        for a, b, c in ((out["Y_proj"][sl], Y[sl], scales[s][0]), (out["tau_proj"][sl], t[sl], scales[s][1]),
+                        (out["B_v"][sl], Bv[sl], scales[s][2]), (out["B_c"][sl], Bc[sl], scales[s][3])):
+            if pinned:
+                # both paths return rounding noise ~eps·cond(J_c) (cond up to 5e8 here): zero to the bar
+                assert np.abs(a).max() <= TOL * c and np.abs(b).max() <= TOL * c, s
+            else:
+                assert rel_floor(a, b, c) < TOL, s
+    G, g, _, _ = ref.normal_equations(Y, t, Bv, Bc)
+    assert rel(out["gram"], G) < TOL and rel(out["Atb"], g) < TOL
+
+
 def test_contact_contract_and_shape_errors():
     model = load_robot("spot")
     d = generate(model, 3, config_index=1)
