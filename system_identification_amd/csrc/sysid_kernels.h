@@ -727,16 +727,17 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       wsync();
     } else {
-      // ---- orthonormal basis of J_c's row space by pivoted modified Gram-Schmidt ----
+      // ---- orthonormal basis of J_c's row space by modified Gram-Schmidt ----
       // P = I - pinv(J_c) J_c is the projector onto null(J_c) = I - Q^T Q for any orthonormal basis Q of
-      // the row space.  Step t takes the row with the largest remaining norm (first on ties) as
-      // q = x_p / |x_p| and removes its direction from every row still in play (lane = row slot, one
-      // wave-synchronous pass per step).  Rows whose remaining norm is <= thr_rel * the largest row norm
-      // are dependent on the taken ones and dropped, as pinv drops singular values <= 1e-15 sigma_max.
-      // The error is ~eps * cond(J_c), pinv's own order (the normal-equations inverse it replaces was
-      // eps * cond^2: 1e-5 at cond 1e6).  q of slot j ends in J_c row j (in place) and, transposed, in
-      // column j of Zt (stride 3 nc); dropped slots are zero in Zt, so P below sums over all k slots.
-      double* nrm = Ms;  // squared remaining norm of each row slot, -1 once taken
+      // the row space.  Row p in turn, if its remaining norm is > thr_rel * the largest row norm, gives
+      // q = x_p / |x_p|, whose direction is removed from every later row (lanes = later rows, one
+      // wave-synchronous pass per row); otherwise it depends on the rows before it and is dropped, as
+      // pinv drops singular values <= 1e-15 sigma_max.  Error ~eps * cond(J_c), pinv's own order (the
+      // normal-equations inverse it replaces was eps * cond^2: 1e-5 at cond 1e6); choosing the largest
+      // remaining row as the next pivot measured no more accurate (tests/test_projector.py) and costs a
+      // k-way argmax per step.  q of slot j ends in J_c row j (in place) and, transposed, in column j of
+      // Zt (stride 3 nc); dropped slots are zero in Zt, so P below sums over all k slots.
+      double* nrm = Ms;  // squared remaining norm of each row slot; -1/|x_p| once taken
       double* Zt = wr + L.Z;
       const int K = 3 * nc;
       for (int j = hl; j < k; j += HW) nrm[j] = mgs_sqnorm<NVC>(Jc + j * nv, nv);
@@ -750,25 +751,19 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         const bool pairs = NVC > 0 && NVC % 2 == 0 && 2 * k <= HW;
         // otherwise lane groups of lpr = 8, 4, 2 or 1 lanes per row, the widest whose rows fit
         const int lpr = 8 * k <= HW ? 8 : (4 * k <= HW ? 4 : (2 * k <= HW ? 2 : 1));
-        for (int t = 0; t < k; ++t) {
-          int p = 0;
-          double best = -1.0;
-          for (int j = 0; j < k; ++j) {
-            const double v = nrm[j];
-            if (v > best) { best = v; p = j; }
-          }
-          if (!(best > thr)) break;  // uniform within the sample's lanes
+        for (int p = 0; p < k; ++p) {
+          const double best = nrm[p];
+          if (!(best > thr)) continue;  // dependent on the rows before it: dropped (uniform per sample)
           const double inv = rsqrt_f64(best);
           const double inv2 = inv * inv;
           const double* xp = Jc + p * nv;
           if constexpr (NVC > 0 && NVC % 2 == 0) {
             if (pairs) {
               const int j = hl >> 1;
-              // taken slots keep their scale as -1/|x_p| (the pivot's row is final: scaled below)
-              const double nj = j < k ? nrm[j] : -1.0;
+              // a taken slot keeps its scale as -1/|x_p| (its row is final: scaled below)
               if (j == p) {
                 if ((hl & 1) == 0) nrm[p] = -inv;
-              } else if (nj >= 0.0) {
+              } else if (j > p && j < k) {
                 const double a = mgs_step_pair<NVC>(xp, Jc + j * NVC, inv2, hl & 1);
                 if ((hl & 1) == 0) nrm[j] = a;
               }
@@ -777,10 +772,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           if (!pairs) {
             if (k * lpr <= HW) {
               const int j = hl / lpr, h = hl - j * lpr;
-              const double nj = j < k ? nrm[j] : -1.0;
               if (j == p) {
                 if (h == 0) nrm[p] = -inv;
-              } else if (nj >= 0.0) {
+              } else if (j > p && j < k) {
                 const double a = mgs_step_group(xp, Jc + j * nv, inv2, nv, h, lpr);
                 if (h == 0) nrm[j] = a;
               }
@@ -788,7 +782,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
               for (int j = hl; j < k; j += HW) {
                 if (j == p) {
                   nrm[p] = -inv;
-                } else if (nrm[j] >= 0.0) {
+                } else if (j > p) {
                   nrm[j] = mgs_step_group(xp, Jc + j * nv, inv2, nv, 0, 1);
                 }
               }

@@ -4,7 +4,7 @@ The kernel does not follow pinocchio's backward pass.  It uses, per sample:
 
 * motion axes of every dof in the base (free-flyer) frame: ``w_r`` (direction) and ``p_r`` (a point);
 * the contact Jacobian from the same axes; ``P = I - Q^T Q`` with the rows of ``Q`` an orthonormal basis of
-  J_c's row space (pivoted modified Gram-Schmidt);
+  J_c's row space (modified Gram-Schmidt);
 * ``H_i = P · M_i · J_w^T`` (nv x 6, world coordinates), built by one rank-1 update per body from its
   parent (``M_i`` = mask of the dofs supporting body i);
 * each regressor column of body i as ``H_i · f^w`` with ``f^w`` the body-regressor column moved to world.
@@ -51,26 +51,23 @@ def contact_jacobian(model, d, cnt, W, Pt, lin):
 
 
 def projector_mgs(Jc, thr_rel=1e-14):
-    """P = I - Q^T Q with the rows of Q an orthonormal basis of J_c's row space by pivoted modified
-    Gram-Schmidt, as K1 computes it: step t takes the row with the largest remaining norm (first on ties),
-    rows whose remaining norm is <= thr_rel * the largest row norm are dropped (pinv's rank cut)."""
+    """P = I - Q^T Q with the rows of Q an orthonormal basis of J_c's row space by modified Gram-Schmidt in
+    row order, as K1 computes it: row p is taken (q = x_p / |x_p|, removed from every later row) when its
+    remaining norm is > thr_rel * the largest row norm, dropped otherwise (pinv's rank cut)."""
     X = np.array(Jc, dtype=np.float64)
     k, nv = X.shape
     nrm = np.einsum("ij,ij->i", X, X)
     thr = thr_rel * thr_rel * (nrm.max() if k else 0.0)
-    scale = np.zeros(k)  # 1/|x_p| of each taken slot; 0 for dropped slots
-    for _ in range(k):
-        p = int(np.argmax(nrm))
+    scale = np.zeros(k)  # 1/|x_p| of each taken row; 0 for dropped rows
+    for p in range(k):
         best = nrm[p]
         if not best > thr:
-            break
+            continue
         inv = 1.0 / np.sqrt(best)
         scale[p] = inv
-        nrm[p] = -1.0
-        for j in range(k):
-            if nrm[j] >= 0.0:
-                X[j] = X[j] - ((X[p] @ X[j]) * (inv * inv)) * X[p]
-                nrm[j] = X[j] @ X[j]
+        for j in range(p + 1, k):
+            X[j] = X[j] - ((X[p] @ X[j]) * (inv * inv)) * X[p]
+            nrm[j] = X[j] @ X[j]
     Q = X * scale[:, None]
     return np.eye(nv) - Q.T @ Q
 

@@ -1,4 +1,4 @@
-"""The contact nullspace projector as K1 computes it (pivoted modified Gram-Schmidt, tests/alg_mirror.py)
+"""The contact nullspace projector as K1 computes it (modified Gram-Schmidt, tests/alg_mirror.py)
 against the reference's ``P = I - pinv(J_c) J_c`` (src/sys_identification.py:131-135, numpy's pinv with its
 default rcond 1e-15).
 
