@@ -442,7 +442,51 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     for (int J0 = I0; J0 < nsg; ++J0) sl.push_back(int2{I0, J0});
   const int per_group = K2_WAVES * K2_SPW;
   e->ngroups = ((int)sl.size() + per_group - 1) / per_group;
-  sl.resize((size_t)e->ngroups * per_group, int2{-1, -1});
+  {
+    // MFMA balance: super-tiles carry 1-4 tiles (diagonal ones skip their lower tile, edge ones the tiles
+    // past the Gram).  The waves of a workgroup share 4 SIMDs (wave w on SIMD w % 4, two waves each), so
+    // super-tiles are dealt largest first to the least loaded group, then SIMD, then wave with a free slot.
+    auto ntiles = [&](int2 t) {
+      int n = 0;
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+          const int I0 = 2 * t.x + a, J0 = 2 * t.y + b;
+          n += (I0 <= J0 && J0 < e->ntc) ? 1 : 0;
+        }
+      return n;
+    };
+    std::vector<int2> order(sl);
+    std::stable_sort(order.begin(), order.end(), [&](int2 a, int2 b) { return ntiles(a) > ntiles(b); });
+    const int nsimd = 4, wps = K2_WAVES / nsimd;  // waves per SIMD
+    std::vector<int2> dealt((size_t)e->ngroups * per_group, int2{-1, -1});
+    std::vector<int> gload(e->ngroups, 0), wload((size_t)e->ngroups * K2_WAVES, 0),
+        wfill((size_t)e->ngroups * K2_WAVES, 0);
+    for (int2 t : order) {
+      const int n = ntiles(t);
+      int g = -1;
+      for (int x = 0; x < e->ngroups; ++x) {
+        int free = 0;
+        for (int w = 0; w < K2_WAVES; ++w) free += K2_SPW - wfill[x * K2_WAVES + w];
+        if (free > 0 && (g < 0 || gload[x] < gload[g])) g = x;
+      }
+      int bw = -1;
+      for (int w = 0; w < K2_WAVES; ++w) {
+        if (wfill[g * K2_WAVES + w] >= K2_SPW) continue;
+        const int sm = w % nsimd;
+        int sl_load = 0;
+        for (int k = 0; k < wps; ++k) sl_load += wload[g * K2_WAVES + sm + nsimd * k];
+        int bl = 0;
+        if (bw >= 0)
+          for (int k = 0; k < wps; ++k) bl += wload[g * K2_WAVES + bw % nsimd + nsimd * k];
+        if (bw < 0 || sl_load < bl || (sl_load == bl && wload[g * K2_WAVES + w] < wload[g * K2_WAVES + bw])) bw = w;
+      }
+      dealt[(size_t)(g * K2_WAVES + bw) * K2_SPW + wfill[g * K2_WAVES + bw]] = t;
+      ++wfill[g * K2_WAVES + bw];
+      wload[g * K2_WAVES + bw] += n;
+      gload[g] += n;
+    }
+    sl.swap(dealt);
+  }
   std::vector<int2> tl(sl.size() * 4, int2{-1, -1});
   for (size_t k = 0; k < sl.size(); ++k) {
     if (sl[k].x < 0) continue;

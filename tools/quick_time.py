@@ -25,3 +25,11 @@ from system_identification_amd import engine as _E
 cfg = (ctypes.c_int32 * 4)()
 eng.lib.sysid_debug_k1_config(eng._h, cfg)
 print("k1 config [waves/block, blocks/CU, lds bytes, maxch]:", list(cfg))
+# whole step as the product runs it (pipelined K1 -> K2 when the panel is large enough)
+for _ in range(3): eng.build_device(din, N, EMIT_ALL, bufs)
+torch.cuda.synchronize()
+t = time.perf_counter()
+for _ in range(20): eng.build_device(din, N, EMIT_ALL, bufs)
+torch.cuda.synchronize()
+st_ms = (time.perf_counter() - t) / 20 * 1e3
+print("step (build_device) %.4f ms  samples/s %.3e  env chunks=%s ks=%s" % (st_ms, N / st_ms * 1e3, os.environ.get("SYSID_PIPE_CHUNKS"), os.environ.get("SYSID_PIPE_KS")))
