@@ -719,6 +719,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     wsync();
 
+    // H1 computed with P by the register-blocked quadruped path (free-flyer dofs 0..5)
+    const bool h1_fused = NVC == 18 && HW == 32 && kp.has_ff && kp.ff0 == 0;
     if (kp.full) {
       // get_full_regressor_force (src/sys_identification.py:391-399): no projection
       for (int e = hl; e < nv * nv; e += HW) {
@@ -803,16 +805,81 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       K1_STAMP(4)
 
       // ---- P = I - Q^T Q  (Zt row a = column a of Q; J_c rows = rows of Q) ----
-      // P's entries are produced row-major, HW per pass, and a pass may overwrite Zt rows that earlier
-      // passes consumed (wave_layout); the ordering point after each pass keeps the passes in order.
-      for (int e = hl; e < nv * nv; e += HW) {
-        const int a = e / nv, b = e - a * nv;
-        const double* za = Zt + a * K;
-        double acc = 0.0;
+      if constexpr (NVC == 18 && HW == 32) {
+        // Register-blocked: lane = (row pair, 6-column group), 27 lanes x 12 entries, every load before
+        // any store, so P may overwrite Zt freely and no ordering point is needed between entries.  The
+        // lanes of column group 0 hold P[a, 0:6] and also write H1 = P[:, ff] J_w[:, ff]^T for their two
+        // rows (over J_c, read completely by then) when the free-flyer's dofs are 0..5.
+        const int rp = hl / 3, cg = hl - 3 * rp;
+        if (hl < 27) {
+          const int a0 = 2 * rp, b0 = 6 * cg;
+          double acc[2][6];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) acc[i][c] = 0.0;
 #pragma unroll 4
-        for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
-        Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+          for (int j = 0; j < k; ++j) {
+            const double z0 = Zt[a0 * K + j], z1 = Zt[(a0 + 1) * K + j];
+            const double2* qr = reinterpret_cast<const double2*>(Jc + j * 18 + b0);
+            const double2 q0 = qr[0], q1 = qr[1], q2 = qr[2];
+            const double qv[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+              acc[0][c] += z0 * qv[c];
+              acc[1][c] += z1 * qv[c];
+            }
+          }
+          double pv[2][6];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) pv[i][c] = (a0 + i == b0 + c ? 1.0 : 0.0) - acc[i][c];
+          const bool h1_here = cg == 0 && h1_fused;
+          double h[2][6];
+          if (h1_here) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+              double j6[6];
+#pragma unroll
+              for (int d = 0; d < 6; ++d) j6[d] = Jws[6 * d + c];
+#pragma unroll
+              for (int i = 0; i < 2; ++i) {
+                double x = 0.0;
+#pragma unroll
+                for (int d = 0; d < 6; ++d) x += pv[i][d] * j6[d];
+                h[i][c] = x;
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            double2* pr = reinterpret_cast<double2*>(Ps + (a0 + i) * 18 + b0);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) pr[c] = make_double2(pv[i][2 * c], pv[i][2 * c + 1]);
+          }
+          if (h1_here) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              double2* hr = reinterpret_cast<double2*>(H1 + (a0 + i) * 6);
+#pragma unroll
+              for (int c = 0; c < 3; ++c) hr[c] = make_double2(h[i][2 * c], h[i][2 * c + 1]);
+            }
+          }
+        }
         wsync();
+      } else {
+        // P's entries are produced row-major, HW per pass, and a pass may overwrite Zt rows that earlier
+        // passes consumed (wave_layout); the ordering point after each pass keeps the passes in order.
+        for (int e = hl; e < nv * nv; e += HW) {
+          const int a = e / nv, b = e - a * nv;
+          const double* za = Zt + a * K;
+          double acc = 0.0;
+#pragma unroll 4
+          for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
+          Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+          wsync();
+        }
       }
     }
     K1_STAMP(5)
@@ -849,7 +916,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       tps[r] = acc;
     }
     if (kp.full) wsync();
-    for (int e = hl; e < nv * 6; e += HW) {
+    for (int e = hl; e < nv * 6 && !(h1_fused && !kp.full); e += HW) {
       const int r = e / 6, c = e - 6 * r;
       double h = 0.0;
       if (kp.has_ff)
