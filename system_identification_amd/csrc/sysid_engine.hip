@@ -126,8 +126,9 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
 enum { K1_C4_NV18, K1_C4, K1_C16 };
 
 // maxch: the longest revolute chain.  The nv = 18 kernel unrolls SYSID_K1_QCH chain slots.
-int k1_variant(int maxch, int nv) {
-  if (maxch <= SYSID_K1_QCH && nv == 18) return K1_C4_NV18;
+int k1_variant(int maxch, int nv, int nbody) {
+  // the nv = 18 kernel stages two panel rows of all bodies (lane = body x row group: 11..16 bodies)
+  if (maxch <= SYSID_K1_QCH && nv == 18 && nbody >= 11 && nbody <= 16) return K1_C4_NV18;
   return maxch <= 4 ? K1_C4 : K1_C16;
 }
 
@@ -421,7 +422,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->ldp = (e->ncol + 1) & ~1;
   e->in_rows = in_rows;
   e->in_lds = in_lds;
-  e->k1_variant = k1_variant(maxch, nv);
+  e->k1_variant = k1_variant(maxch, nv, NJ - 1);
   const WLay WL = wave_layout(in_lds, nv, NJ, nc, k1_layout_hw(e->k1_variant));
   K1Params& kp = e->kp;
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;

@@ -942,58 +942,103 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
-    // One G row (6 + 6*chain FMAs) feeds 42 FMAs and five 16-byte stores.  (Staging the rows through
-    // LDS to make the stores contiguous measured 17% slower: the store path is not the limiter.)
+    // One G row (6 + 6*chain FMAs) feeds 42 FMAs.
     double* out = panel + ((s + half) * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
-    for (int it = hl; it < nyi && valid; it += HW) {
-      const int g = it / nbody, i = it - g * nbody + 1;
-      const int r0 = g * nv / kp.rg, r1 = (g + 1) * nv / kp.rg;
-      double F[FBLK];
-      body_regressor_block(body + BODY_STRIDE * i, F);
-      const int cl = chain_len[i];
-      int dof[MAXCH];  // the chain's dofs, read once: no dependent index load per row
+    auto block_row = [&](int r, const double* F, const int* dof, int cl, double* y) {
+      const double* h = H1 + 6 * r;
+      const double* pr = Ps + r * nv;
+      double G[6];
 #pragma unroll
-      for (int t = 0; t < MAXCH; ++t) dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
-      double* oi = out + 10 * (i - 1);
-      for (int r = r0; r < r1; ++r) {
-        const double* h = H1 + 6 * r;
-        const double* pr = Ps + r * nv;
-        double G[6];
+      for (int k = 0; k < 6; ++k) G[k] = h[k];
+      if constexpr (CHAIN_UNCOND) {
+        // unconditional loads (dof[t] = 0 past the chain is a valid slot), masked products
 #pragma unroll
-        for (int k = 0; k < 6; ++k) G[k] = h[k];
-        if constexpr (CHAIN_UNCOND) {
-          // unconditional loads (dof[t] = 0 past the chain is a valid slot), masked products
+        for (int t = 0; t < MAXCH; ++t) {
+          const double pl = pr[dof[t]];
+          const double pv = t < cl ? pl : 0.0;
+          const double* jw = Jws + 6 * dof[t];
 #pragma unroll
-          for (int t = 0; t < MAXCH; ++t) {
-            const double pl = pr[dof[t]];
-            const double pv = t < cl ? pl : 0.0;
+          for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < MAXCH; ++t) {
+          if (t < cl) {
+            const double pv = pr[dof[t]];
             const double* jw = Jws + 6 * dof[t];
 #pragma unroll
             for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
           }
-        } else {
+        }
+      }
 #pragma unroll
-          for (int t = 0; t < MAXCH; ++t) {
-            if (t < cl) {
-              const double pv = pr[dof[t]];
-              const double* jw = Jws + 6 * dof[t];
+      for (int c = 0; c < 4; ++c)
+        y[c] = G[0] * F[6 * c] + G[1] * F[6 * c + 1] + G[2] * F[6 * c + 2] + G[3] * F[6 * c + 3] +
+               G[4] * F[6 * c + 4] + G[5] * F[6 * c + 5];
 #pragma unroll
-              for (int k = 0; k < 6; ++k) G[k] += pv * jw[k];
-            }
+      for (int c = 0; c < 6; ++c)
+        y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
+    };
+    auto block_setup = [&](int i, double* F, int* dof) {
+      body_regressor_block(body + BODY_STRIDE * i, F);
+      const int cl = chain_len[i];
+#pragma unroll
+      for (int t = 0; t < MAXCH; ++t) dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
+      return cl;
+    };
+#ifndef SYSID_STAGE_Y
+#define SYSID_STAGE_Y 1
+#endif
+    // Quadrupeds: the rg = 2 row groups' current rows are staged in LDS over the joint records (dead
+    // once every lane holds its block F) and written out as whole contiguous panel rows: one 16-byte
+    // store per lane per 512 contiguous bytes instead of 16-byte pieces 80 bytes apart.
+    // (The host picks this kernel only for 11..16 bodies: rg = 2 row groups, nyi <= 32 lanes, and the two
+    // staged rows fit in the joint records.)
+    if constexpr (SYSID_STAGE_Y && NVC == 18 && HW == 32) {
+      constexpr int RH = NVC / 2;  // rows per row group
+      const bool act = hl < nyi && valid;
+      const int g = hl / nbody, i = hl - g * nbody + 1;  // lanes past nyi compute a real body's block
+      double F[FBLK];
+      int dof[MAXCH];
+      const int cl = block_setup(i, F, dof);
+      wsync();  // every read of the joint records precedes the first staging store
+      double* stg = body;  // [row group][wy]
+      const int wy2 = kp.wy >> 1, n2 = kp.rg * wy2;
+#pragma unroll 1
+      for (int rho = 0; rho < RH; ++rho) {
+        if (act) {
+          double y[10];
+          block_row(g * RH + rho, F, dof, cl, y);
+          double2* sp = reinterpret_cast<double2*>(stg + g * kp.wy + 10 * (i - 1));
+#pragma unroll
+          for (int c = 0; c < 5; ++c) sp[c] = make_double2(y[2 * c], y[2 * c + 1]);
+        }
+        wsync();
+        if (valid) {
+          const double2* s2 = reinterpret_cast<const double2*>(stg);
+          for (int x = hl; x < n2; x += HW) {
+            const int gg = x >= wy2 ? 1 : 0, c2 = x - gg * wy2;
+            panel_store(reinterpret_cast<double2*>(out + (int64_t)(gg * RH + rho) * ldp) + c2, s2[x]);
           }
         }
-        double y[10];
+        wsync();
+      }
+    } else {
+      for (int it = hl; it < nyi && valid; it += HW) {
+        const int g = it / nbody, i = it - g * nbody + 1;
+        const int r0 = g * nv / kp.rg, r1 = (g + 1) * nv / kp.rg;
+        double F[FBLK];
+        int dof[MAXCH];  // the chain's dofs, read once: no dependent index load per row
+        const int cl = block_setup(i, F, dof);
+        double* oi = out + 10 * (i - 1);
+        for (int r = r0; r < r1; ++r) {
+          double y[10];
+          block_row(r, F, dof, cl, y);
+          double2* o2 = reinterpret_cast<double2*>(oi + (int64_t)r * ldp);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          y[c] = G[0] * F[6 * c] + G[1] * F[6 * c + 1] + G[2] * F[6 * c + 2] + G[3] * F[6 * c + 3] +
-                 G[4] * F[6 * c + 4] + G[5] * F[6 * c + 5];
-#pragma unroll
-        for (int c = 0; c < 6; ++c)
-          y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
-        double2* o2 = reinterpret_cast<double2*>(oi + (int64_t)r * ldp);
-#pragma unroll
-        for (int c = 0; c < 5; ++c) panel_store(o2 + c, make_double2(y[2 * c], y[2 * c + 1]));
+          for (int c = 0; c < 5; ++c) panel_store(o2 + c, make_double2(y[2 * c], y[2 * c + 1]));
+        }
       }
     }
 
