@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32", "bf16"],
                     help="Gram arithmetic for --gram-only (f32/bf16: config 5 throughput, error reported)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="extra all-core C oracle timing (0 = off)")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                    help="threads of the extra all-core C oracle timing (0 = off; 16 = the GPU box's CPU share)")
     return ap.parse_args()
 
 
@@ -61,15 +62,27 @@ def pmc_traffic(kernel, robot, samples):
     return None, None
 
 
-def cpu_baseline(model, data, n_sample):
-    """The C restatement of the reference path (oracle/sysid_oracle.c), one thread, on n_sample samples."""
+def cpu_baseline(model, data, n_sample, nthreads=1):
+    """The C restatement of the reference path (oracle/sysid_oracle.c) on n_sample samples (OpenMP over the
+    samples when nthreads > 1)."""
     from oracle.ref_c import COracle
     o = COracle(model)
     sl = {k: data[k][:, :n_sample].copy() for k in ("q", "dq", "ddq", "tau", "contact")}
     t0 = time.perf_counter()
-    o.build(sl["q"], sl["dq"], sl["ddq"], sl["tau"], sl["contact"], nthreads=1)
+    o.build(sl["q"], sl["dq"], sl["ddq"], sl["tau"], sl["contact"], nthreads=nthreads)
     dt = time.perf_counter() - t0
     return n_sample / dt, dt
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def main():
@@ -183,21 +196,21 @@ def main():
         "K1_GBps": round(k1_gbs, 1), "K2_TFps": round(k2_tfs, 3),
         "roofline": roof,
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N = 1 only
         n_cpu = min(N, 20000)
         v, dt = cpu_baseline(model, data, n_cpu)
         result["cpu_baseline"] = {
             "value": round(v, 1), "unit": "samples/s", "cores": 1, "kind": "port",
             "sample": f"{n_cpu} {args.robot} samples, oracle/sysid_oracle.c single thread: reference structure "
                       f"(2 FK passes + 2 SVD pinv per sample, stacking, AᵀA), {dt:.2f} s",
+            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count(),
+                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")},
         }
-        if args.cpu_threads > 0:
-            from oracle.ref_c import COracle
-            o = COracle(model)
-            t0 = time.perf_counter()
-            o.build(data["q"], data["dq"], data["ddq"], data["tau"], data["contact"], nthreads=args.cpu_threads)
-            result["cpu_baseline_allcores"] = {"value": round(N / (time.perf_counter() - t0), 1),
-                                               "cores": args.cpu_threads}
+        if args.cpu_threads > 1:
+            v2, dt2 = cpu_baseline(model, data, n_cpu, nthreads=args.cpu_threads)
+            result["cpu_baseline_allcores"] = {
+                "value": round(v2, 1), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
+                "sample": f"the same {n_cpu} samples, oracle/sysid_oracle.c with OpenMP over the samples, {dt2:.2f} s"}
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -241,6 +241,14 @@ __device__ __forceinline__ double group_sum(double v, int lpr) {
   return v;
 }
 
+// v of lane `lane` (a wave-uniform index) in every lane.
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // |x|^2 of a row of nv doubles (three partial sums).
 template <int NVC>
 __device__ __forceinline__ double mgs_sqnorm(const double* x, int nv_rt) {
@@ -686,8 +694,10 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         pfs[3 * c] = x[0] + bj[9]; pfs[3 * c + 1] = x[1] + bj[10]; pfs[3 * c + 2] = x[2] + bj[11];
       }
     }
-    int na = 0;
-    for (int c = 0; c < nc; ++c) na += cnt[c] != 0.0 ? 1 : 0;
+    // contacts with a non-zero value as a bit mask (independent loads, no search loop per entry below)
+    unsigned long long amask = 0ull;
+    for (int c = 0; c < nc; ++c) amask |= (cnt[c] != 0.0 ? 1ull : 0ull) << c;
+    const int na = __popcll(amask);
     const int k = 3 * na;
     wsync();
     K1_STAMP(2)
@@ -695,11 +705,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // ---- contact Jacobian (LOCAL_WORLD_ALIGNED, linear rows) ----
     for (int e = hl; e < k * nv; e += HW) {
       const int rho = e / nv, r = e - rho * nv;
-      int c = 0;
-      for (int seen = -1; c < nc; ++c) {  // the (rho/3)-th contact with a non-zero value
-        seen += cnt[c] != 0.0 ? 1 : 0;
-        if (seen == rho / 3) break;
-      }
+      unsigned long long m = amask;  // the (rho/3)-th contact with a non-zero value
+      for (int t = rho / 3; t > 0; --t) m &= m - 1ull;
+      const int c = __ffsll((long long)m) - 1;
       const int comp = rho - 3 * (rho / 3);
       double val = 0.0;
       if ((csupp[c] >> r) & 1ull) {
@@ -742,65 +750,137 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       double* nrm = Ms;  // squared remaining norm of each row slot; -1/|x_p| once taken
       double* Zt = wr + L.Z;
       const int K = 3 * nc;
-      for (int j = hl; j < k; j += HW) nrm[j] = mgs_sqnorm<NVC>(Jc + j * nv, nv);
-      wsync();
-      K1_STAMP(3)
-      {
-        double nmax = 0.0;
-        for (int j = 0; j < k; ++j) nmax = fmax(nmax, nrm[j]);
-        const double thr = kp.thr_rel * kp.thr_rel * nmax;
-        // lane pairs per row for the compile-time-nv kernel when the rows fit (uniform per sample)
-        const bool pairs = NVC > 0 && NVC % 2 == 0 && 2 * k <= HW;
-        // otherwise lane groups of lpr = 8, 4, 2 or 1 lanes per row, the widest whose rows fit
-        const int lpr = 8 * k <= HW ? 8 : (4 * k <= HW ? 4 : (2 * k <= HW ? 2 : 1));
-        for (int p = 0; p < k; ++p) {
-          const double best = nrm[p];
-          if (!(best > thr)) continue;  // dependent on the rows before it: dropped (uniform per sample)
-          const double inv = rsqrt_f64(best);
-          const double inv2 = inv * inv;
-          const double* xp = Jc + p * nv;
-          if constexpr (NVC > 0 && NVC % 2 == 0) {
-            if (pairs) {
-              const int j = hl >> 1;
-              // a taken slot keeps its scale as -1/|x_p| (its row is final: scaled below)
-              if (j == p) {
-                if ((hl & 1) == 0) nrm[p] = -inv;
-              } else if (j > p && j < k) {
-                const double a = mgs_step_pair<NVC>(xp, Jc + j * NVC, inv2, hl & 1);
-                if ((hl & 1) == 0) nrm[j] = a;
-              }
-            }
-          }
-          if (!pairs) {
-            if (k * lpr <= HW) {
-              const int j = hl / lpr, h = hl - j * lpr;
-              if (j == p) {
-                if (h == 0) nrm[p] = -inv;
-              } else if (j > p && j < k) {
-                const double a = mgs_step_group(xp, Jc + j * nv, inv2, nv, h, lpr);
-                if (h == 0) nrm[j] = a;
-              }
-            } else {
-              for (int j = hl; j < k; j += HW) {
+      // Generic form: rows in LDS, lane groups per row, the norms through LDS.
+      auto mgs_lds = [&]() {
+        for (int j = hl; j < k; j += HW) nrm[j] = mgs_sqnorm<NVC>(Jc + j * nv, nv);
+        wsync();
+        K1_STAMP(3)
+        {
+          double nmax = 0.0;
+          for (int j = 0; j < k; ++j) nmax = fmax(nmax, nrm[j]);
+          const double thr = kp.thr_rel * kp.thr_rel * nmax;
+          // lane pairs per row for the compile-time-nv kernel when the rows fit (uniform per sample)
+          const bool pairs = NVC > 0 && NVC % 2 == 0 && 2 * k <= HW;
+          // otherwise lane groups of lpr = 8, 4, 2 or 1 lanes per row, the widest whose rows fit
+          const int lpr = 8 * k <= HW ? 8 : (4 * k <= HW ? 4 : (2 * k <= HW ? 2 : 1));
+          for (int p = 0; p < k; ++p) {
+            const double best = nrm[p];
+            if (!(best > thr)) continue;  // dependent on the rows before it: dropped (uniform per sample)
+            const double inv = rsqrt_f64(best);
+            const double inv2 = inv * inv;
+            const double* xp = Jc + p * nv;
+            if constexpr (NVC > 0 && NVC % 2 == 0) {
+              if (pairs) {
+                const int j = hl >> 1;
+                // a taken slot keeps its scale as -1/|x_p| (its row is final: scaled below)
                 if (j == p) {
-                  nrm[p] = -inv;
-                } else if (j > p) {
-                  nrm[j] = mgs_step_group(xp, Jc + j * nv, inv2, nv, 0, 1);
+                  if ((hl & 1) == 0) nrm[p] = -inv;
+                } else if (j > p && j < k) {
+                  const double a = mgs_step_pair<NVC>(xp, Jc + j * NVC, inv2, hl & 1);
+                  if ((hl & 1) == 0) nrm[j] = a;
                 }
               }
             }
+            if (!pairs) {
+              if (k * lpr <= HW) {
+                const int j = hl / lpr, h = hl - j * lpr;
+                if (j == p) {
+                  if (h == 0) nrm[p] = -inv;
+                } else if (j > p && j < k) {
+                  const double a = mgs_step_group(xp, Jc + j * nv, inv2, nv, h, lpr);
+                  if (h == 0) nrm[j] = a;
+                }
+              } else {
+                for (int j = hl; j < k; j += HW) {
+                  if (j == p) {
+                    nrm[p] = -inv;
+                  } else if (j > p) {
+                    nrm[j] = mgs_step_group(xp, Jc + j * nv, inv2, nv, 0, 1);
+                  }
+                }
+              }
+            }
+            wsync();
+          }
+          // q of each taken slot = its row x 1/|x_p| (in place, and transposed into Zt); dropped slots: 0
+          for (int e = hl; e < k * nv; e += HW) {
+            const int j = e / nv, r = e - j * nv;
+            const double sc = nrm[j] < 0.0 ? -nrm[j] : 0.0;
+            const double qv = Jc[e] * sc;
+            Jc[e] = qv;
+            Zt[r * K + j] = qv;
           }
           wsync();
         }
-        // q of each taken slot = its row x 1/|x_p| (in place, and transposed into Zt); dropped slots: 0
-        for (int e = hl; e < k * nv; e += HW) {
-          const int j = e / nv, r = e - j * nv;
-          const double sc = nrm[j] < 0.0 ? -nrm[j] : 0.0;
-          const double qv = Jc[e] * sc;
-          Jc[e] = qv;
-          Zt[r * K + j] = qv;
+      };
+      if constexpr (NVC == 18 && HW == 32) {
+        if (2 * k <= HW) {
+          // Quadruped form: lane pair (2j, 2j+1) keeps its half-row of row j in registers through every
+          // step; the pivot's norm comes from its lanes by readlane (no LDS round trip per step) and only
+          // the pivot's half-row is read from LDS; an updated row is written back for its own turn.
+          constexpr int H = ((NVC + 1) / 2 + 1) & ~1, H2 = H / 2;
+          const int j = hl >> 1, h = hl & 1;
+          const int n2 = h == 0 ? H2 : (NVC - H) / 2;
+          const bool row = j < k;
+          double2* xrow = reinterpret_cast<double2*>(Jc + (row ? j : 0) * NVC + h * H);
+          double2 xv[H2];
+          double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+          for (int u = 0; u < H2; ++u) {
+            xv[u] = (row && u < n2) ? xrow[u] : make_double2(0.0, 0.0);
+            a0 += xv[u].x * xv[u].x;
+            a1 += xv[u].y * xv[u].y;
+          }
+          double myn = pair_sum(a0 + a1);
+          if (row && h == 0) nrm[j] = myn;
+          wsync();
+          K1_STAMP(3)
+          double nmax = 0.0;
+          for (int jj = 0; jj < k; ++jj) nmax = fmax(nmax, nrm[jj]);
+          const double thr = kp.thr_rel * kp.thr_rel * nmax;
+          double sc = 0.0;  // 1/|x_j| once row j is taken; 0 if it is dropped
+          for (int p = 0; p < k; ++p) {
+            const double n0 = readlane_f64(myn, 2 * p), n1 = readlane_f64(myn, HW + 2 * p);
+            const double best = half ? n1 : n0;
+            if (!(best > thr)) continue;  // dependent on the rows before it: dropped
+            const double inv = rsqrt_f64(best);
+            if (j == p) sc = inv;
+            if (row && j > p) {
+              const double2* xp = reinterpret_cast<const double2*>(Jc + p * NVC + h * H);
+              double2 pv[H2];
+              double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+              for (int u = 0; u < H2; ++u) {
+                pv[u] = u < n2 ? xp[u] : make_double2(0.0, 0.0);
+                c0 += pv[u].x * xv[u].x;
+                c1 += pv[u].y * xv[u].y;
+              }
+              const double c = pair_sum(c0 + c1) * (inv * inv);
+              double b0 = 0.0, b1 = 0.0;
+#pragma unroll
+              for (int u = 0; u < H2; ++u) {
+                xv[u].x -= c * pv[u].x;
+                xv[u].y -= c * pv[u].y;
+                b0 += xv[u].x * xv[u].x;
+                b1 += xv[u].y * xv[u].y;
+                if (u < n2) xrow[u] = xv[u];
+              }
+              myn = pair_sum(b0 + b1);
+            }
+            wsync();
+          }
+          // Q rows = x_j / |x_j| (taken) or 0 (dropped), in place: P below reads Q from J_c
+          if (row) {
+#pragma unroll
+            for (int u = 0; u < H2; ++u)
+              if (u < n2) xrow[u] = make_double2(xv[u].x * sc, xv[u].y * sc);
+          }
+          wsync();
+        } else {
+          mgs_lds();
         }
-        wsync();
+      } else {
+        mgs_lds();
       }
       K1_STAMP(4)
 
@@ -820,7 +900,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
             for (int c = 0; c < 6; ++c) acc[i][c] = 0.0;
 #pragma unroll 4
           for (int j = 0; j < k; ++j) {
-            const double z0 = Zt[a0 * K + j], z1 = Zt[(a0 + 1) * K + j];
+            const double2 zz = *reinterpret_cast<const double2*>(Jc + j * 18 + a0);  // Q[j][a0], Q[j][a0+1]
+            const double z0 = zz.x, z1 = zz.y;
             const double2* qr = reinterpret_cast<const double2*>(Jc + j * 18 + b0);
             const double2 q0 = qr[0], q1 = qr[1], q2 = qr[2];
             const double qv[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
@@ -869,8 +950,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
         wsync();
       } else {
-        // P's entries are produced row-major, HW per pass, and a pass may overwrite Zt rows that earlier
-        // passes consumed (wave_layout); the ordering point after each pass keeps the passes in order.
+        // Runtime-nv kernels: P has its own region (wave_layout with hw = 0), so its passes need no
+        // ordering point between them.
         for (int e = hl; e < nv * nv; e += HW) {
           const int a = e / nv, b = e - a * nv;
           const double* za = Zt + a * K;
@@ -878,8 +959,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll 4
           for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
           Ps[e] = (a == b ? 1.0 : 0.0) - acc;
-          wsync();
         }
+        wsync();
       }
     }
     K1_STAMP(5)

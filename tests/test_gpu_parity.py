@@ -122,6 +122,22 @@ def test_ill_conditioned_contact_jacobians():
     assert rel(out["gram"], G) < TOL and rel(out["Atb"], g) < TOL
 
 
+def test_exactly_dependent_contact_rows():
+    """Two contact slots on one foot frame (Spot with end-effector 1 := end-effector 0): with both in contact
+    J_c repeats three rows exactly; pinv drops them, and so must the quadruped kernel's Gram-Schmidt."""
+    import copy
+    model = copy.deepcopy(load_robot("spot"))
+    model.end_effector_names[1] = model.end_effector_names[0]
+    N = 16
+    d = generate(model, N, config_index=2)
+    cnt = np.ones((4, N))
+    cnt[2:, ::2] = 0.0
+    out = Engine(model).build(d["q"], d["dq"], d["ddq"], d["tau"], cnt, EMIT_ALL)
+    Y, t = ref.get_projected_y_tau(model, d["q"], d["dq"], d["ddq"], d["tau"], cnt)
+    Bv, Bc = ref.get_projected_friction_regressors(model, d["q"], d["dq"], d["ddq"], cnt)
+    check_blocks(out, Y, t, Bv, Bc, model, d["q"], d["dq"], d["ddq"], d["tau"])
+
+
 def test_contact_contract_and_shape_errors():
     model = load_robot("spot")
     d = generate(model, 3, config_index=1)
