@@ -427,6 +427,9 @@ template <int MAXCH, int NVC, int SPW>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
 #endif
+#ifndef SYSID_PRIO
+#define SYSID_PRIO 1  // column phase at low issue priority, the latency-bound phases high (K1 -2%)
+#endif
 // Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
 __global__ void __launch_bounds__(64 * K1_WAVES, SPW == 2 ? 2 : SYSID_K1_MIN_WAVES_PER_EU)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
@@ -537,6 +540,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
+#if SYSID_PRIO
+  __builtin_amdgcn_s_setprio(2);
+#endif
   const int hl_outer = hl;
   while (s < N) {
     // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
@@ -1020,6 +1026,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     K1_STAMP(6)
 
+#if SYSID_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
@@ -1144,6 +1153,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         panel_store(reinterpret_cast<double2*>(out + (int64_t)r * ldp + kp.wy + 2 * m), make_double2(v2[0], v2[1]));
       }
     }
+#if SYSID_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#endif
     K1_STAMP(7)
     s = s1;
     s1 = s2;
