@@ -588,6 +588,62 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // ---- forward pass (computeJointTorqueRegressor forward step) + placements ----
     // Joint placements liMi = jointPlacement * M_J(q) of every joint at once (one lane per joint: the
     // sincos / quaternion work is off the depth-serial path), parked in the joint's own pose slot.
+    // Forward step of joint j from its parent's record (its liMi is in its own record, from the placement
+    // pass below).
+    auto level_step = [&](int j) {
+      const int p = parent[j];
+      const int iv = idx_v[j];
+      const double* bp = body + BODY_STRIDE * p;
+      double* bj = body + BODY_STRIDE * j;
+      double liR[9], lit[3], vJ[6], Sa[6];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) liR[k] = bj[k];
+      lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
+      const bool ff = jtype[j] == JT_FREEFLYER;
+      if (ff) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { vJ[k] = dq[iv + k]; Sa[k] = ddq[iv + k]; }
+      } else {
+        const double* ax = axis + 3 * j;
+        const double w = dq[iv], aa = ddq[iv];
+        vJ[0] = vJ[1] = vJ[2] = 0.0; Sa[0] = Sa[1] = Sa[2] = 0.0;
+        vJ[3] = ax[0] * w; vJ[4] = ax[1] * w; vJ[5] = ax[2] * w;
+        Sa[3] = ax[0] * aa; Sa[4] = ax[1] * aa; Sa[5] = ax[2] * aa;
+      }
+      double vp[6], ap[6], vi[6], ai[6], c1[3], c2[3];
+      act_inv_motion(liR, lit, bp + 12, vp);
+      act_inv_motion(liR, lit, bp + 18, ap);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) vi[k] = vJ[k] + vp[k];
+      if (ff) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ai[k] = Sa[k] + ap[k];  // v x v = 0
+      } else {
+        cross3(vi, vJ + 3, c1);      // motion cross v x vJ with vJ = (0, wJ)
+        cross3(vi + 3, vJ + 3, c2);
+        ai[0] = c1[0] + Sa[0] + ap[0]; ai[1] = c1[1] + Sa[1] + ap[1]; ai[2] = c1[2] + Sa[2] + ap[2];
+        ai[3] = c2[0] + Sa[3] + ap[3]; ai[4] = c2[1] + Sa[4] + ap[4]; ai[5] = c2[2] + Sa[5] + ap[5];
+      }
+      // Poses are kept relative to the free-flyer (base) frame, not the world: the regressor rows of
+      // pinocchio only see the base rotation through R_b^T g (its actInv above), and J_c's row space
+      // (hence P) is the same in base-aligned and world-aligned axes because R_b is invertible.  This
+      // stays exact for the float32, slightly non-unit quaternions of the reference's .dat logs.
+      double oR[9], ot[3];
+      if (ff) {
+        oR[0] = 1.0; oR[1] = 0.0; oR[2] = 0.0; oR[3] = 0.0; oR[4] = 1.0; oR[5] = 0.0;
+        oR[6] = 0.0; oR[7] = 0.0; oR[8] = 1.0;
+        ot[0] = ot[1] = ot[2] = 0.0;
+      } else {
+        mat3mul(bp, liR, oR);
+        mat3vec(bp, lit, ot);
+        ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) bj[k] = oR[k];
+      bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { bj[12 + k] = vi[k]; bj[18 + k] = ai[k]; }
+    };
     for (int j = 1 + hl; j < NJ; j += HW) {
       const int iq = idx_q[j];
       double RJ[9], tJ[3];
@@ -603,65 +659,14 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       mat3mul(R0 + 9 * j, RJ, bj);
       mat3vec(R0 + 9 * j, tJ, tmp);
       bj[9] = tmp[0] + t0[3 * j]; bj[10] = tmp[1] + t0[3 * j + 1]; bj[11] = tmp[2] + t0[3 * j + 2];
+      if (depth[j] == 1) level_step(j);
     }
     wsync();
-    // Velocities / accelerations level by level (a joint's parent is one level up).
-    for (int lvl = 1; lvl <= kp.maxdepth; ++lvl) {
-      for (int j = 1 + hl; j < NJ; j += HW) {
-        if (depth[j] != lvl) continue;
-        const int p = parent[j];
-        const int iv = idx_v[j];
-        const double* bp = body + BODY_STRIDE * p;
-        double* bj = body + BODY_STRIDE * j;
-        double liR[9], lit[3], vJ[6], Sa[6];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) liR[k] = bj[k];
-        lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
-        const bool ff = jtype[j] == JT_FREEFLYER;
-        if (ff) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) { vJ[k] = dq[iv + k]; Sa[k] = ddq[iv + k]; }
-        } else {
-          const double* ax = axis + 3 * j;
-          const double w = dq[iv], aa = ddq[iv];
-          vJ[0] = vJ[1] = vJ[2] = 0.0; Sa[0] = Sa[1] = Sa[2] = 0.0;
-          vJ[3] = ax[0] * w; vJ[4] = ax[1] * w; vJ[5] = ax[2] * w;
-          Sa[3] = ax[0] * aa; Sa[4] = ax[1] * aa; Sa[5] = ax[2] * aa;
-        }
-        double vp[6], ap[6], vi[6], ai[6], c1[3], c2[3];
-        act_inv_motion(liR, lit, bp + 12, vp);
-        act_inv_motion(liR, lit, bp + 18, ap);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) vi[k] = vJ[k] + vp[k];
-        if (ff) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) ai[k] = Sa[k] + ap[k];  // v x v = 0
-        } else {
-          cross3(vi, vJ + 3, c1);      // motion cross v x vJ with vJ = (0, wJ)
-          cross3(vi + 3, vJ + 3, c2);
-          ai[0] = c1[0] + Sa[0] + ap[0]; ai[1] = c1[1] + Sa[1] + ap[1]; ai[2] = c1[2] + Sa[2] + ap[2];
-          ai[3] = c2[0] + Sa[3] + ap[3]; ai[4] = c2[1] + Sa[4] + ap[4]; ai[5] = c2[2] + Sa[5] + ap[5];
-        }
-        // Poses are kept relative to the free-flyer (base) frame, not the world: the regressor rows of
-        // pinocchio only see the base rotation through R_b^T g (its actInv above), and J_c's row space
-        // (hence P) is the same in base-aligned and world-aligned axes because R_b is invertible.  This
-        // stays exact for the float32, slightly non-unit quaternions of the reference's .dat logs.
-        double oR[9], ot[3];
-        if (ff) {
-          oR[0] = 1.0; oR[1] = 0.0; oR[2] = 0.0; oR[3] = 0.0; oR[4] = 1.0; oR[5] = 0.0;
-          oR[6] = 0.0; oR[7] = 0.0; oR[8] = 1.0;
-          ot[0] = ot[1] = ot[2] = 0.0;
-        } else {
-          mat3mul(bp, liR, oR);
-          mat3vec(bp, lit, ot);
-          ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
-        }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) bj[k] = oR[k];
-        bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) { bj[12 + k] = vi[k]; bj[18 + k] = ai[k]; }
-      }
+    // Velocities / accelerations level by level (a joint's parent is one level up); level 1 (parent = the
+    // universe, whose record is set at the top of the step) runs in the placement pass.
+    for (int lvl = 2; lvl <= kp.maxdepth; ++lvl) {
+      for (int j = 1 + hl; j < NJ; j += HW)
+        if (depth[j] == lvl) level_step(j);
       wsync();
     }
     K1_STAMP(1)
