@@ -47,7 +47,12 @@ def pmc_traffic(kernel, robot, samples):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary for this workload
     (profiles/<round>/pmc_summary.json: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+    import re
+
+    def version(path):  # r01_v10 sorts after r01_v9: compare the numbers, not the strings
+        return [int(n) for n in re.findall(r"\d+", os.path.basename(os.path.dirname(path)))]
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), key=version, reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
