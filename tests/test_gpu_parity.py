@@ -218,6 +218,36 @@ def test_full_size_properties(robot, N):
         assert rel(rows, A) < TOL
 
 
+@pytest.mark.parametrize("robot,N", [("spot", 3000), ("g1_29dof", 700)])
+def test_hip_graph_replay_matches_eager(robot, N):
+    """The device entry points are stream-ordered and allocation-free: one step captured into a HIP graph
+    (what bench.py replays) gives bitwise the eager results, replay after replay, full and Gram-only."""
+    import torch
+    model = load_robot(robot)
+    e = eng(robot)
+    d = generate(model, N, config_index=6)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_device(N, EMIT_ALL)
+    gb = e.alloc_gram_device(N)
+    e.build_device(din, N, EMIT_ALL, bufs)
+    e.build_gram_device(din, N, gb)
+    torch.cuda.synchronize()
+    W = e.w
+    P, G, GO = bufs["panel"][: N * e.nv, : W + 1], bufs["gram"][: W + 1, : W + 1], gb["gram"][: W + 1, : W + 1]
+    p0, g0, go0 = P.clone(), G.clone(), GO.clone()
+    for t in (P, G, GO):  # the graph must rewrite every element the reference reads
+        t.fill_(float("nan"))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        st = torch.cuda.current_stream().cuda_stream
+        e.build_device(din, N, EMIT_ALL, bufs, stream=st)
+        e.build_gram_device(din, N, gb, stream=st)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(p0, P) and torch.equal(g0, G) and torch.equal(go0, GO)
+
+
 @pytest.mark.parametrize("robot,N", [("spot", 50000), ("g1_29dof", 12000)])
 def test_gram_only_chunked(robot, N):
     """Gram-only path (panel produced in ~512 MiB chunks on the device, several chunks here) against
