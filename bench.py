@@ -1,13 +1,16 @@
 """Benchmark: regressor + projector + Gram build on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--robot spot] [--samples 20000] [--gram-only]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--robot spot] [--samples 20000 | --total-samples T]
+                    [--gram-only [--precision f64|f32|bf16]] [--no-cpu-baseline] [--no-e2e] [--graph]
 
 One "step" = one pass of the hot path over one batch of synthetic samples already resident in HBM:
 K1 (per-sample regressor Y, contact projector P, stacked [Y_proj | B_v | B_c | tau_proj] panel written
 to HBM in the reference's row layout) + K2/K3 (Gram AᵀA, Aᵀb, bᵀb on fp64 MFMA) + for N > 1 one RCCL
-all-reduce of the Gram.  Samples are sharded: every rank processes its own --samples (weak scaling).
+all-reduce of the Gram through the engine's own C-ABI exchange (sysid_allreduce_gram).  Samples are
+sharded: with --samples every rank processes its own batch (weak scaling); with --total-samples the job's
+samples are split over the ranks (strong scaling, BASELINE config 4: --total-samples 200000).
 Rank 0 prints one JSON line.  For N > 1 launch with
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N ...
 """
 import argparse
@@ -23,6 +26,7 @@ METRIC = "regressor samples/sec + Gram-build GF/s, 12-DoF, 20k samples, 1/2/4/8 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_MFMA_PEAK_TFS = 78.6  # AMD public spec for MI355X fp64 matrix (not in the container guide)
 MFMA_PEAK_TFS = {"f64": FP64_MFMA_PEAK_TFS, "f32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md (dense)
+BOX_CPU_SHARE = 16        # host threads a one-GPU box grants a job (OMP_NUM_THREADS there)
 
 
 def parse():
@@ -31,17 +35,22 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--robot", default="spot")
-    ap.add_argument("--samples", type=int, default=20000, help="samples per GPU")
+    ap.add_argument("--samples", type=int, default=20000, help="samples per GPU (weak scaling)")
+    ap.add_argument("--total-samples", type=int, default=0,
+                    help="samples of the whole job, split over the ranks (strong scaling; config 4 = 200000)")
     ap.add_argument("--gram-only", action="store_true",
                     help="normal equations only (SURVEY.md §8d config 5): the panel is produced chunk by chunk on "
                          "the device and never returned")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32", "bf16"],
                     help="Gram arithmetic for --gram-only (f32/bf16: config 5 throughput, error reported)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) legs")
     ap.add_argument("--graph", action="store_true",
                     help="replay one captured HIP graph per step instead of eager launches (measured no gain)")
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
-                    help="threads of the extra all-core C oracle timing (0 = off; 16 = the GPU box's CPU share)")
+    ap.add_argument("--cpu-threads", type=int, default=BOX_CPU_SHARE,
+                    help="threads of the extra multi-core C oracle timing (0 = off; 16 = the GPU box's CPU share)")
+    ap.add_argument("--ref-samples", type=int, default=2000,
+                    help="samples of the numpy reference-structure CPU leg (0 = off)")
     return ap.parse_args()
 
 
@@ -81,6 +90,23 @@ def cpu_baseline(model, data, n_sample, nthreads=1):
     return n_sample / dt, dt
 
 
+def cpu_reference_structure(model, data, n_sample):
+    """BASELINE.md CPU leg (i): the reference's own loop structure — per-sample get_proj_regressor_torque and
+    get_proj_friction_regressors (two FK passes, two SVD pinvs per sample), np.vstack / np.hstack
+    (demo/spot_identification.py:37-56, 84-87) and AᵀA — with pinocchio's algorithms restated in numpy
+    (oracle/ref_numpy.py), on one core (BLAS limited to one thread)."""
+    from threadpoolctl import threadpool_limits
+    from oracle import ref_numpy as ref
+    sl = {k: data[k][:, :n_sample].copy() for k in ("q", "dq", "ddq", "tau", "contact")}
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        Y, t = ref.get_projected_y_tau(model, sl["q"], sl["dq"], sl["ddq"], sl["tau"], sl["contact"])
+        Bv, Bc = ref.get_projected_friction_regressors(model, sl["q"], sl["dq"], sl["ddq"], sl["contact"])
+        ref.normal_equations(Y, t, Bv, Bc)
+        dt = time.perf_counter() - t0
+    return n_sample / dt, dt
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -90,6 +116,28 @@ def cpu_model():
     except OSError:
         pass
     return None
+
+
+def e2e_legs(eng, data, N, reps=3):
+    """§8(d) end-to-end samples/s of the host entry point (numpy in -> numpy out, PCIe both ways):
+    full outputs (stacked Y_proj, tau_proj, B_v, B_c + Gram) and Gram only (inputs in, 190 KB out)."""
+    from system_identification_amd.engine import EMIT_ALL, EMIT_GRAM
+    ins = [data[k] for k in ("q", "dq", "ddq", "tau", "contact")]
+    in_bytes = sum(a.nbytes for a in ins)
+    res = {}
+    for name, flags in (("full", EMIT_ALL), ("gram_only", EMIT_GRAM)):
+        eng.build(*ins, flags)  # warm: device buffers grown once
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            out = eng.build(*ins, flags)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out_bytes = sum(v.nbytes for v in out.values() if hasattr(v, "nbytes"))
+        res[name] = {"samples_per_s": round(N / best, 1), "ms": round(best * 1e3, 3),
+                     "pcie_bytes": int(in_bytes + out_bytes),
+                     "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 2)}
+    return res
 
 
 def main():
@@ -108,44 +156,56 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from system_identification_amd.engine import EMIT_ALL, Engine
+    from system_identification_amd.distributed import RcclGramComm, shard_range
+    from system_identification_amd.engine import EMIT_ALL, GRAM_PRECISION, Engine
     from system_identification_amd.model import load_robot
     from system_identification_amd.synthetic import channel_block, generate
 
     model = load_robot(args.robot)
-    N = args.samples
+    strong = args.total_samples > 0
+    if strong:
+        s0, s1 = shard_range(args.total_samples, rank, world)
+        N = s1 - s0
+        total_per_step = args.total_samples
+    else:
+        N = args.samples
+        total_per_step = N * world
     data = generate(model, N, config_index=1 + rank)  # each rank its own shard of the log
     eng = Engine(model, device=local)
     d_in = torch.from_numpy(channel_block(data)).cuda(local)
-    from system_identification_amd.engine import GRAM_PRECISION
     flags = EMIT_ALL
     tflags = EMIT_ALL | (GRAM_PRECISION[args.precision] if args.gram_only else 0)  # kernels timed below
     stream = torch.cuda.current_stream(local)
+
+    comm = None
+    if world > 1:
+        # the engine's own exchange step (C ABI: sysid_rccl_unique_id / _comm_init / sysid_allreduce_gram); the
+        # 128-byte RCCL id travels from rank 0 over the torch process group
+        def share_id(raw):
+            box = [raw if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            return box[0]
+        comm = RcclGramComm(eng, rank, world, share_id=share_id)
+
     if args.gram_only:
         bufs = eng.alloc_gram_device(N)
 
-        def step():
-            eng.build_gram_device(d_in, N, bufs, stream=stream.cuda_stream, precision=args.precision)
-            if world > 1:
-                dist.all_reduce(bufs["gram"])
+        def launch(s):
+            eng.build_gram_device(d_in, N, bufs, stream=s, precision=args.precision)
     else:
         bufs = eng.alloc_device(N, flags)
 
-        def step():
-            eng.build_device(d_in, N, flags, bufs, stream=stream.cuda_stream)
-            if world > 1:
-                dist.all_reduce(bufs["gram"])
+        def launch(s):
+            eng.build_device(d_in, N, flags, bufs, stream=s)
 
-    # One step's launches (memset + K1 + K2 + K3) captured once into a HIP graph and replayed: the same
+    def exchange():
+        if comm is not None:
+            comm.allreduce_gram(bufs["gram"], stream=stream.cuda_stream)
+
+    # One step's launches (memsets + K1 + K2 + K3) captured once into a HIP graph and replayed: the same
     # kernels over the same buffers, without the per-launch host gaps.  The RCCL all-reduce stays eager.
     graph_used = False
     if args.graph:
-        if args.gram_only:
-            def launch(s):
-                eng.build_gram_device(d_in, N, bufs, stream=s, precision=args.precision)
-        else:
-            def launch(s):
-                eng.build_device(d_in, N, flags, bufs, stream=s)
         launch(stream.cuda_stream)  # warm the engine (first-launch setup outside the capture)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -155,8 +215,11 @@ def main():
 
         def step():
             g.replay()
-            if world > 1:
-                dist.all_reduce(bufs["gram"])
+            exchange()
+    else:
+        def step():
+            launch(stream.cuda_stream)
+            exchange()
 
     for _ in range(args.warmup):
         step()
@@ -187,7 +250,9 @@ def main():
     else:
         ms = eng.time_stages(d_in, N, flags, bufs, iters=max(5, args.steps))
     nv, W = model.nv, eng.w
-    bytes_k1 = (model.nq + 2 * nv + model.nj + model.n_ee) * 8 + nv * (W + 1) * 8   # SURVEY §8d per sample
+    in_b = (model.nq + 2 * nv + model.nj + model.n_ee) * 8
+    panel_b = nv * (W + 1) * 8
+    bytes_k1 = in_b + panel_b                                                       # SURVEY §8d per sample
     flops_k2 = nv * W * (W + 1) + 2 * nv * W                                       # SYRK + Aᵀb per sample
     k1_gbs = n_time * bytes_k1 / (ms[0] * 1e-3) / 1e9
     k2_tfs = n_time * flops_k2 / (ms[1] * 1e-3) / 1e12
@@ -205,41 +270,67 @@ def main():
                 "traffic": traffic, "traffic_source": src, "algorithmic_flops_per_launch": n_time * flops_k2,
                 "avg_launch_ms": round(ms[1], 5)}
 
-    total_samples = N * world * args.steps
-    value = total_samples / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    # step-level floor: the bytes the step must move (inputs + panel written by K1 and read back by K2; Gram-only
+    # chunks may stay on-die and are not counted) at HBM peak, and the Gram flops at the MFMA peak
+    step_bytes = N * (in_b + (0 if args.gram_only else 2 * panel_b))
+    hbm_floor = step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
+    mfma_floor = N * flops_k2 / (MFMA_PEAK_TFS[args.precision if args.gram_only else "f64"] * 1e12) * 1e3
+    value = total_per_step * args.steps / elapsed
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "hip_graph": graph_used,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 5),
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+        "hip_graph": graph_used,
         "dtype": "f64" if not args.gram_only or args.precision == "f64" else f"f64 panel, {args.precision} Gram",
         "data": "synthetic (SURVEY.md §8d recipe: sinusoidal joints in URDF limits, wobbling base, "
                 "inverse-dynamics torques + noise, trot contacts with LOST=2); no .dat ships with the reference",
-        "config": {"workload": f"{args.robot} {N} samples per GPU, " + (
+        "config": {"workload": f"{args.robot} " + (f"{args.total_samples} samples split over {world} GPU(s)" if strong
+                                                    else f"{N} samples per GPU") + ", " + (
                        f"Gram only (panel chunked on the device, {args.precision} Gram)" if args.gram_only else
                        "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
-                   "robot": args.robot, "samples_per_gpu": N,
-                   "nv": nv, "W": W, "parallelism": f"dp{world}"},
-        "gram_gflops": round(N * world * flops_k2 / (elapsed / args.steps) / 1e9, 2),
+                   "robot": args.robot, "samples_per_gpu": N, "total_samples_per_step": total_per_step,
+                   "nv": nv, "W": W, "parallelism": f"dp{world}",
+                   "exchange": "sysid_allreduce_gram (RCCL, C ABI)" if world > 1 else None},
+        "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
         "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},
         "K1_GBps": round(k1_gbs, 1), "K2_TFps": round(k2_tfs, 3),
         "roofline": roof,
+        "step_roofline": {"hbm_bytes": step_bytes, "hbm_floor_ms": round(hbm_floor, 5),
+                          "mfma_floor_ms": round(mfma_floor, 5), "floor_ms": round(max(hbm_floor, mfma_floor), 5),
+                          "frac": round(max(hbm_floor, mfma_floor) / ms_step, 4)},
     }
+    if rank == 0 and world == 1 and not args.no_e2e:
+        # PCIe-inclusive host entry point (sysid_build): never the headline value (Measurement)
+        result["e2e"] = e2e_legs(eng, data, N)
+        result["e2e_full_samples_per_s"] = result["e2e"]["full"]["samples_per_s"]
+        result["e2e_gram_only_samples_per_s"] = result["e2e"]["gram_only"]["samples_per_s"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N = 1 only
         n_cpu = min(N, 20000)
         v, dt = cpu_baseline(model, data, n_cpu)
+        host = {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
         result["cpu_baseline"] = {
             "value": round(v, 1), "unit": "samples/s", "cores": 1, "kind": "port",
             "sample": f"{n_cpu} {args.robot} samples, oracle/sysid_oracle.c single thread: reference structure "
-                      f"(2 FK passes + 2 SVD pinv per sample, stacking, AᵀA), {dt:.2f} s",
-            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count(),
-                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")},
-        }
+                      f"(2 FK passes + 2 SVD pinv per sample, stacking, AᵀA), {dt:.2f} s", "host": host}
         if args.cpu_threads > 1:
             v2, dt2 = cpu_baseline(model, data, n_cpu, nthreads=args.cpu_threads)
-            result["cpu_baseline_allcores"] = {
+            result["cpu_baseline_multicore"] = {
                 "value": round(v2, 1), "unit": "samples/s", "cores": args.cpu_threads, "kind": "port",
-                "sample": f"the same {n_cpu} samples, oracle/sysid_oracle.c with OpenMP over the samples, {dt2:.2f} s"}
+                "sample": f"the same {n_cpu} samples, oracle/sysid_oracle.c with OpenMP over the samples on "
+                          f"{args.cpu_threads} threads = the GPU box's CPU share (os.cpu_count() = {os.cpu_count()} "
+                          f"is the whole host), {dt2:.2f} s"}
+        if args.ref_samples > 0:
+            n_ref = min(N, args.ref_samples)
+            v3, dt3 = cpu_reference_structure(model, data, n_ref)
+            result["cpu_baseline_reference_structure"] = {
+                "value": round(v3, 1), "unit": "samples/s", "cores": 1, "kind": "port",
+                "sample": f"{n_ref} {args.robot} samples: the reference's per-sample Python loop "
+                          "(demo/spot_identification.py:37-56, 84-87) over oracle/ref_numpy.py (pinocchio restated "
+                          f"in numpy; BLAS 1 thread) + AᵀA, {dt3:.2f} s"}
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

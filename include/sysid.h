@@ -23,9 +23,14 @@
  *     numpy broadcast error there) with SYSID_E_CONTACT.
  *   - Return codes: 0 = OK, < 0 = error; nothing is thrown across the ABI.  sysid_last_error() gives
  *     a message.  Python maps E_INVALID/E_MODEL/E_CONTACT to ValueError, E_DEVICE/E_NOMEM to RuntimeError.
- *   - A handle is bound to one device and owns one HIP stream; it is not re-entrant across threads,
- *     and at most one of its device launches may be in flight at a time (its K1 sample counter is
- *     per handle): stream-order the calls of one handle, use one handle per concurrent stream.
+ *   - A handle is bound to one device and owns one HIP stream.  The host-buffer entry points (sysid_build,
+ *     sysid_build_full, sysid_tau_error) use buffers owned by the handle: they are synchronous and not
+ *     re-entrant (one thread at a time per handle).  The device entry points keep every piece of per-launch
+ *     state in the caller's workspace (K1's sample counter is its first 256 bytes, zeroed on the launch
+ *     stream before each launch): launches of one handle on different streams with different workspaces may
+ *     run concurrently, and an aborted launch leaves nothing behind for the next one.
+ *   - Every argument check of an entry point happens before its first enqueue: an error return means that
+ *     nothing was enqueued (also under graph capture).
  *
  * Packed model (produced by system_identification_amd.model.Model.pack()), little endian:
  *   int32  header[16] = {0x44495953 'SYID', version 1, nq, nv, njoints, n_contact, base_dof, nj, 0...}
@@ -73,7 +78,7 @@ extern "C" {
 typedef struct sysid_engine sysid_engine;
 
 /* ABI version (bumped on any signature or layout change). */
-int32_t sysid_abi_version(void);  /* 4 */
+int32_t sysid_abi_version(void);  /* 5 */
 
 /* Create an engine for one device from a packed model.  Replaces the model construction of
  * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
@@ -108,7 +113,8 @@ int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, con
                          const double* tau, const double* ee_force, const double* cnt, int64_t N, int64_t ld,
                          double* Y, double* F);
 
-/* Device workspace needed by sysid_build_device for N samples (bytes, 256-B aligned pieces). */
+/* Device workspace needed by sysid_build_device for N samples (bytes; > 0 for every N > 0): the K1 sample
+ * counter, plus the Gram split-K slabs with SYSID_EMIT_GRAM.  The workspace must be 256-byte aligned. */
 size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags);
 
 /* Device-buffer entry point (stream-ordered, no host synchronisation, no allocation: graph-capturable).

@@ -32,6 +32,11 @@ thread_local std::string g_thread_error = "";
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Every device workspace starts with K1's sample counter (one 256-byte piece).  It is zeroed on the launch
+// stream right before each K1 launch, so launches are independent of each other: an aborted launch leaves
+// nothing behind, and launches on different streams with different workspaces may run concurrently.
+constexpr size_t WORK_BYTES = 256;
+
 }  // namespace
 
 struct sysid_engine {
@@ -42,7 +47,7 @@ struct sysid_engine {
   // K1
   K1Params kp{};
   uint32_t* d_mimg = nullptr;
-  unsigned long long* d_work = nullptr;  // K1 sample counter + departed-wave counter (self-resetting)
+  unsigned long long* d_work = nullptr;  // K1 sample counter of the host-API paths (engine-owned buffers)
   int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4, k1_variant = 0;
   size_t k1_lds = 0;
   // K2/K3 Gram tiling
@@ -56,6 +61,9 @@ struct sysid_engine {
   double* d_gram = nullptr;
   void* d_ws = nullptr;
   size_t ws_cap = 0;
+  double* d_out = nullptr;   // host API: de-interleaved stacked outputs (grow-only)
+  size_t out_cap = 0;
+  int host_register = -1;    // host API copies: 1 page-lock the caller's arrays, 0 pageable, -1 by size
   double* d_dump = nullptr;  // diagnostics only
   std::string err;
 };
@@ -146,8 +154,9 @@ const void* k1_fn(int variant) {
 }
 
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
-              hipStream_t st, double* dbg, int full = 0) {
+              unsigned long long* work, hipStream_t st, double* dbg, int full = 0) {
   K1Params kp = e->kp;
+  HIP_TRY(e, hipMemsetAsync(work, 0, 2 * sizeof(unsigned long long), st));
   if (full) {
     kp.full = 1;
     kp.in_rows = e->in_lds;
@@ -162,15 +171,15 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
   switch (e->k1_variant) {
     case K1_C4_NV18:
       hipLaunchKernelGGL((k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N,
-                         ld, d_panel, ld_panel, e->d_work, dbg);
+                         ld, d_panel, ld_panel, work, dbg);
       break;
     case K1_C4:
       hipLaunchKernelGGL((k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
-                         ld_panel, e->d_work, dbg);
+                         ld_panel, work, dbg);
       break;
     default:
       hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
-                         ld_panel, e->d_work, dbg);
+                         ld_panel, work, dbg);
   }
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
@@ -223,22 +232,41 @@ int launch_k3(sysid_engine* e, int ks, const double* slab, double* part, double*
   return SYSID_OK;
 }
 
+// Workspace of sysid_build_device: [K1 counter | K2 slabs | K3 partials] (the last two with EMIT_GRAM).
+size_t stages_ws_bytes(const sysid_engine* e, int64_t N, uint32_t flags) {
+  if (N <= 0) return 0;
+  const int64_t rows = N * e->nv;
+  return WORK_BYTES + ((flags & SYSID_EMIT_GRAM) ? slab_bytes(e, rows) + part_bytes(e, rows) : 0);
+}
+
+// Every check of a launch sequence happens before its first enqueue: an error return means nothing was
+// enqueued (no half-written panel behind an error, no half-recorded graph under capture).
+int check_stages(sysid_engine* e, int64_t N, int64_t ld_panel, uint32_t flags, const void* d_ws, size_t ws_bytes) {
+  const size_t need = stages_ws_bytes(e, N, flags);
+  if (need > 0 && (d_ws == nullptr || ws_bytes < need))
+    return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0, need);
+  if ((flags & SYSID_EMIT_GRAM) && ld_panel > 16 * e->ntc)
+    return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
+  if (reinterpret_cast<uintptr_t>(d_ws) & 255)
+    return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
+  return SYSID_OK;
+}
+
 int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                   int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, hipStream_t st,
                   hipEvent_t* ev /* 4 events or null */) {
   if (N <= 0) return SYSID_OK;
-  const int64_t rows = N * e->nv;
-  if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
-  int rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, st, nullptr);
+  int rc = check_stages(e, N, ld_panel, flags, d_ws, ws_bytes);
   if (rc != SYSID_OK) return rc;
+  const int64_t rows = N * e->nv;
+  auto* work = static_cast<unsigned long long*>(d_ws);
+  if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
+  if ((rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, work, st, nullptr)) != SYSID_OK) return rc;
   if (ev) HIP_TRY(e, hipEventRecord(ev[1], st));
   if (flags & SYSID_EMIT_GRAM) {
     const int ks = ksplit_for(e, rows);
-    const size_t sb = slab_bytes(e, rows), pb = part_bytes(e, rows);
-    if (d_ws == nullptr || ws_bytes < sb + pb)
-      return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, sb + pb);
-    double* slab = static_cast<double*>(d_ws);
-    double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + sb);
+    double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
+    double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows));
     if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
     if ((rc = launch_k3(e, ks, slab, part, d_gram, st)) != SYSID_OK) return rc;
@@ -258,29 +286,69 @@ int64_t gram_chunk(const sysid_engine* e, int64_t N) {
   return std::max<int64_t>(1, std::min(c, N));
 }
 
+// [K1 counter | panel chunk | K2 slabs | K3 partials]
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {
   const int64_t rows = gram_chunk(e, N) * e->nv;
-  return align256((size_t)rows * e->ldp * sizeof(double)) + slab_bytes(e, rows) + part_bytes(e, rows);
+  return WORK_BYTES + align256((size_t)rows * e->ldp * sizeof(double)) + slab_bytes(e, rows) + part_bytes(e, rows);
 }
 
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st) {
   if (N <= 0) return SYSID_OK;
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes(e, N))
-    return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", ws_bytes, gram_ws_bytes(e, N));
+    return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
+                   gram_ws_bytes(e, N));
+  if (reinterpret_cast<uintptr_t>(d_ws) & 255) return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
   const int64_t C = gram_chunk(e, N), rows0 = C * e->nv;
-  double* panel = static_cast<double*>(d_ws);
-  double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + align256((size_t)rows0 * e->ldp * sizeof(double)));
+  auto* work = static_cast<unsigned long long*>(d_ws);
+  double* panel = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
+  double* slab = reinterpret_cast<double*>(reinterpret_cast<char*>(panel) + align256((size_t)rows0 * e->ldp * sizeof(double)));
   double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows0));
   const int ks0 = ksplit_for(e, rows0);
   int rc;
   for (int64_t c0 = 0; c0 < N; c0 += C) {
     const int64_t n = std::min(C, N - c0);
-    if ((rc = launch_k1(e, d_in + c0, n, ld, panel, e->ldp, st, nullptr)) != SYSID_OK) return rc;
+    if ((rc = launch_k1(e, d_in + c0, n, ld, panel, e->ldp, work, st, nullptr)) != SYSID_OK) return rc;
     const int ks = std::min(ks0, ksplit_for(e, n * e->nv));
     if ((rc = launch_k2(e, panel, n * e->nv, e->ldp, ks, c0 > 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
   }
   return launch_k3(e, ks0, slab, part, d_gram, st);
+}
+
+// Host <-> device copies of the host entry points.  The caller's numpy arrays are pageable; a large copy
+// page-locks the destination in place for its duration (hipHostRegister), so the DMA engine writes it
+// directly instead of bouncing through the runtime's pinned staging buffers.  Memory that is already
+// pinned is copied as is.  Returns the host ranges registered here (unregistered after the stream sync).
+constexpr size_t REGISTER_MIN_BYTES = 8u << 20;
+
+int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st,
+              std::vector<void*>* registered) {
+  if (bytes == 0) return SYSID_OK;
+  void* host = kind == hipMemcpyDeviceToHost ? dst : const_cast<void*>(src);
+  const bool want = e->host_register > 0 || (e->host_register < 0 && bytes >= REGISTER_MIN_BYTES);
+  if (want) {
+    const hipError_t r = hipHostRegister(host, bytes, hipHostRegisterDefault);
+    if (r == hipSuccess) registered->push_back(host);
+    else (void)hipGetLastError();  // already pinned, or not registrable: the plain copy below still works
+  }
+  HIP_TRY(e, hipMemcpyAsync(dst, src, bytes, kind, st));
+  return SYSID_OK;
+}
+
+int host_unregister(sysid_engine* e, std::vector<void*>& registered) {
+  for (void* p : registered) (void)hipHostUnregister(p);
+  registered.clear();
+  (void)e;
+  return SYSID_OK;
+}
+
+int launch_k5(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_panel, double* Y, double* tau,
+              double* Bv, double* Bc, hipStream_t st) {
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, (int64_t)e->cus * 8));
+  hipLaunchKernelGGL(k5_unstack, dim3((unsigned)blocks), dim3(256), 0, st, d_panel, rows, ld_panel, e->wy, e->nj, Y,
+                     tau, Bv, Bc);
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
 }
 
 int k4_blocks(const sysid_engine* e, int64_t N) {
@@ -306,7 +374,7 @@ int launch_k4(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t 
 
 extern "C" {
 
-int32_t sysid_abi_version(void) { return 4; }
+int32_t sysid_abi_version(void) { return 5; }
 
 const char* sysid_last_error(const sysid_engine* e) { return e ? e->err.c_str() : g_thread_error.c_str(); }
 
@@ -509,6 +577,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
   if (st == hipSuccess) st = hipMalloc(&e->d_work, 2 * sizeof(unsigned long long));
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, 2 * sizeof(unsigned long long));
   if (st == hipSuccess) st = hipMalloc(&e->d_tiles, both.size() * sizeof(int2));
@@ -548,7 +617,7 @@ void sysid_destroy(sysid_engine* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->d_tiles, (void*)e->d_in, (void*)e->d_panel,
-                  (void*)e->d_gram, e->d_ws, (void*)e->d_dump})
+                  (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -568,9 +637,8 @@ int32_t sysid_dims(const sysid_engine* e, int32_t* nq, int32_t* nv, int32_t* nj,
 }
 
 size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags) {
-  if (!e || N <= 0 || !(flags & SYSID_EMIT_GRAM)) return 0;
-  const int64_t rows = N * e->nv;
-  return slab_bytes(e, rows) + part_bytes(e, rows);
+  if (!e) return 0;
+  return stages_ws_bytes(e, N, flags);
 }
 
 int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld, int64_t* bad) {
@@ -692,7 +760,7 @@ int32_t sysid_tau_error(sysid_engine* e, const double* q, const double* dq, cons
   double* d_phi = reinterpret_cast<double*>(static_cast<char*>(e->d_ws) + sysid_tau_error_workspace_bytes(e, N));
   double* d_err = d_phi + e->wy;
   HIP_TRY(e, hipMemcpyAsync(d_phi, phi, (size_t)e->wy * sizeof(double), hipMemcpyHostToDevice, st));
-  if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, st, nullptr)) != SYSID_OK) return rc;
+  if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, e->d_work, st, nullptr)) != SYSID_OK) return rc;
   if ((rc = launch_k4(e, e->d_panel, e->ldp, N, d_phi, d_err, e->d_ws, sysid_tau_error_workspace_bytes(e, N), st)))
     return rc;
   HIP_TRY(e, hipMemcpyAsync(err_sq, d_err, (size_t)e->nv * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -738,7 +806,7 @@ int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, con
                                   hipMemcpyHostToDevice, st));
     r0 += nrows[k];
   }
-  if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, st, nullptr, 1)) != SYSID_OK) return rc;
+  if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, e->d_work, st, nullptr, 1)) != SYSID_OK) return rc;
   const size_t pitch = (size_t)e->ldp * sizeof(double);
   if (Y)
     HIP_TRY(e, hipMemcpy2DAsync(Y, (size_t)e->wy * sizeof(double), e->d_panel, pitch, (size_t)e->wy * sizeof(double),
@@ -808,44 +876,62 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const size_t wsb = gram_only ? gram_ws_bytes(e, N) : sysid_workspace_bytes(e, N, flags);
   if ((rc = grow(e, &e->d_ws, &e->ws_cap, wsb ? wsb : 256))) return rc;
   hipStream_t st = e->stream;
-  const size_t rowb = (size_t)N * sizeof(double);
+  std::vector<void*> reg;
+  auto fail = [&](int code) { (void)hipStreamSynchronize(st); host_unregister(e, reg); return code; };
+  // inputs: channel c of the caller's arrays -> row c of the device block (one copy per array when ld == N)
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
   int64_t r0 = 0;
   for (int k = 0; k < 5; ++k) {
-    if (nrows[k] > 0)
-      HIP_TRY(e, hipMemcpy2DAsync(e->d_in + r0 * N, rowb, srcs[k], (size_t)ld * sizeof(double), rowb, nrows[k],
-                                  hipMemcpyHostToDevice, st));
+    if (nrows[k] > 0) {
+      if (ld == N) {
+        if ((rc = host_copy(e, e->d_in + r0 * N, srcs[k], (size_t)nrows[k] * N * sizeof(double),
+                            hipMemcpyHostToDevice, st, &reg)) != SYSID_OK)
+          return fail(rc);
+      } else if (hipMemcpy2DAsync(e->d_in + r0 * N, (size_t)N * sizeof(double), srcs[k], (size_t)ld * sizeof(double),
+                                  (size_t)N * sizeof(double), nrows[k], hipMemcpyHostToDevice, st) != hipSuccess) {
+        return fail(set_err(e, SYSID_E_DEVICE, "input copy failed"));
+      }
+    }
     r0 += nrows[k];
   }
   rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
-  if (rc != SYSID_OK) return rc;
-  const size_t pitch = (size_t)e->ldp * sizeof(double);
-  if (Y_proj && (flags & SYSID_EMIT_Y))
-    HIP_TRY(e, hipMemcpy2DAsync(Y_proj, (size_t)e->wy * sizeof(double), e->d_panel, pitch, (size_t)e->wy * sizeof(double),
-                                rows, hipMemcpyDeviceToHost, st));
-  if (tau_proj && (flags & SYSID_EMIT_TAU))
-    HIP_TRY(e, hipMemcpy2DAsync(tau_proj, sizeof(double), e->d_panel + e->w, pitch, sizeof(double), rows,
-                                hipMemcpyDeviceToHost, st));
-  if (flags & SYSID_EMIT_FRICTION) {
-    if (B_v && e->nj)
-      HIP_TRY(e, hipMemcpy2DAsync(B_v, (size_t)e->nj * sizeof(double), e->d_panel + e->wy, pitch,
-                                  (size_t)e->nj * sizeof(double), rows, hipMemcpyDeviceToHost, st));
-    if (B_c && e->nj)
-      HIP_TRY(e, hipMemcpy2DAsync(B_c, (size_t)e->nj * sizeof(double), e->d_panel + e->wy + e->nj, pitch,
-                                  (size_t)e->nj * sizeof(double), rows, hipMemcpyDeviceToHost, st));
+  if (rc != SYSID_OK) return fail(rc);
+  if (panel_out) {
+    // de-interleave the requested outputs on the device, then one contiguous copy per output
+    const bool wY = Y_proj && (flags & SYSID_EMIT_Y), wT = tau_proj && (flags & SYSID_EMIT_TAU);
+    const bool wV = B_v && (flags & SYSID_EMIT_FRICTION) && e->nj, wC = B_c && (flags & SYSID_EMIT_FRICTION) && e->nj;
+    const size_t nY = wY ? (size_t)rows * e->wy : 0, nT = wT ? (size_t)rows : 0;
+    const size_t nV = wV ? (size_t)rows * e->nj : 0, nC = wC ? (size_t)rows * e->nj : 0;
+    if ((rc = grow(e, reinterpret_cast<void**>(&e->d_out), &e->out_cap, (nY + nT + nV + nC) * sizeof(double) + 64)))
+      return fail(rc);
+    double* dY = e->d_out;
+    double* dT = dY + nY;
+    double* dV = dT + nT;
+    double* dC = dV + nV;
+    if ((rc = launch_k5(e, e->d_panel, rows, e->ldp, wY ? dY : nullptr, wT ? dT : nullptr, wV ? dV : nullptr,
+                        wC ? dC : nullptr, st)) != SYSID_OK)
+      return fail(rc);
+    const struct { double* h; const double* d; size_t n; } outs[4] = {{Y_proj, dY, nY}, {tau_proj, dT, nT},
+                                                                       {B_v, dV, nV}, {B_c, dC, nC}};
+    for (const auto& o : outs)
+      if (o.n && (rc = host_copy(e, o.h, o.d, o.n * sizeof(double), hipMemcpyDeviceToHost, st, &reg)) != SYSID_OK)
+        return fail(rc);
   }
   if (want_gram) {
     const size_t W = (size_t)e->w;
-    if (gram)
-      HIP_TRY(e, hipMemcpy2DAsync(gram, W * sizeof(double), e->d_gram, (size_t)e->ncol * sizeof(double),
-                                  W * sizeof(double), W, hipMemcpyDeviceToHost, st));
-    if (Atb) HIP_TRY(e, hipMemcpyAsync(Atb, e->d_gram + W * e->ncol, W * sizeof(double), hipMemcpyDeviceToHost, st));
-    if (btb)
-      HIP_TRY(e, hipMemcpyAsync(btb, e->d_gram + W * e->ncol + W, sizeof(double), hipMemcpyDeviceToHost, st));
+    if (gram && hipMemcpy2DAsync(gram, W * sizeof(double), e->d_gram, (size_t)e->ncol * sizeof(double),
+                                 W * sizeof(double), W, hipMemcpyDeviceToHost, st) != hipSuccess)
+      return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
+    if (Atb && hipMemcpyAsync(Atb, e->d_gram + W * e->ncol, W * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
+      return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
+    if (btb && hipMemcpyAsync(btb, e->d_gram + W * e->ncol + W, sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
+      return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
   }
-  HIP_TRY(e, hipStreamSynchronize(st));
+  const hipError_t sst = hipStreamSynchronize(st);
+  host_unregister(e, reg);
+  if (sst != hipSuccess) return set_err(e, SYSID_E_DEVICE, "stream sync failed: %s", hipGetErrorString(sst));
   return SYSID_OK;
 }
 
@@ -890,7 +976,7 @@ int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, cons
                        nullptr, nullptr);  // allocates the device buffers
   if (rc != SYSID_OK) return rc;
   HIP_TRY(e, hipMalloc(&e->d_dump, (size_t)L.total * sizeof(double)));
-  rc = launch_k1(e, e->d_in, 1, 1, e->d_panel, e->ldp, e->stream, e->d_dump);
+  rc = launch_k1(e, e->d_in, 1, 1, e->d_panel, e->ldp, e->d_work, e->stream, e->d_dump);
   if (rc == SYSID_OK && hipStreamSynchronize(e->stream) != hipSuccess) rc = set_err(e, SYSID_E_DEVICE, "sync failed");
   if (rc == SYSID_OK &&
       hipMemcpy(lds_image, e->d_dump, (size_t)L.total * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
@@ -915,7 +1001,7 @@ int32_t sysid_debug_stamps(sysid_engine* e, const double* d_in, int64_t N, int64
   HIP_TRY(e, hipSetDevice(e->device));
   HIP_TRY(e, hipMalloc(&e->d_dump, 16 * sizeof(uint64_t)));
   HIP_TRY(e, hipMemset(e->d_dump, 0, 16 * sizeof(uint64_t)));
-  int rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, e->stream, e->d_dump);
+  int rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, e->d_work, e->stream, e->d_dump);
   HIP_TRY(e, hipStreamSynchronize(e->stream));
   HIP_TRY(e, hipMemcpy(out16, e->d_dump, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   (void)hipFree(e->d_dump);
@@ -931,15 +1017,15 @@ int32_t sysid_exp_k2(sysid_engine* e, const double* d_panel, int64_t N, int64_t 
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t rows = N * e->nv;
   const int ks = ksplit_for(e, rows);
-  double* slab = static_cast<double*>(d_ws);
-  double* part = reinterpret_cast<double*>(static_cast<char*>(d_ws) + slab_bytes(e, rows));
+  double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
+  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows));
   int rc = launch_k2(e, d_panel, rows, ld_panel, ks, accumulate, slab, st, 0);
   if (rc == SYSID_OK && final) rc = launch_k3(e, ks, slab, part, d_gram, st);
   return rc;
 }
 int32_t sysid_exp_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
                      void* stream) {
-  return launch_k1(e, d_in, N, ld, d_panel, ld_panel, static_cast<hipStream_t>(stream), nullptr);
+  return launch_k1(e, d_in, N, ld, d_panel, ld_panel, e->d_work, static_cast<hipStream_t>(stream), nullptr);
 }
 #endif
 

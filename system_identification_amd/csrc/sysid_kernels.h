@@ -321,8 +321,23 @@ __device__ __forceinline__ double mgs_step_pair(const double* xp, double* x, dou
   return pair_sum(a0 + a1);
 }
 
-// Panel stores (plain: non-temporal stores measured equal on Spot and 2.5x slower K1 on G1).
-__device__ __forceinline__ void panel_store(double2* p, double2 v) { *p = v; }
+// Panel stores (plain: non-temporal stores measured equal on Spot and 2.5x slower K1 on G1).  Two adjacent
+// columns per store, in the panel's element type: f64 (the reference's outputs and the parity Gram) or, for
+// the Gram-only chunk panel of a reduced-precision Gram, f32 / bf16 — rounded once
+// here, so the Gram kernel stages 2x / 4x fewer bytes than from an f64 panel.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void panel_store(double* p, double a, double b) {
+  *reinterpret_cast<double2*>(p) = make_double2(a, b);
+}
+__device__ __forceinline__ void panel_store(float* p, double a, double b) {
+  *reinterpret_cast<float2*>(p) = make_float2((float)a, (float)b);
+}
+__device__ __forceinline__ void panel_store(__bf16* p, double a, double b) {
+  bf16x2_t v;
+  v[0] = (__bf16)(float)a;  // RNE to f32, then RNE to bf16 (v_cvt_pk_bf16_f32)
+  v[1] = (__bf16)(float)b;
+  *reinterpret_cast<bf16x2_t*>(p) = v;
+}
 
 #ifdef SYSID_STAMPS
 // Diagnostics build: per-phase shader-clock deltas accumulated in registers (s_memtime is uniform, so
@@ -423,7 +438,7 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 // SPW: samples per wave (1 or 2).  With SPW > 1 each 64/SPW-lane slice of the wave carries its own
 // sample through every phase, so the lane-starved serial phases (forward pass, Gram-Schmidt steps) do SPW
 // samples per instruction; each slice has its own LDS region.
-template <int MAXCH, int NVC, int SPW>
+template <int MAXCH, int NVC, int SPW, typename OutT>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
 #endif
@@ -433,7 +448,7 @@ template <int MAXCH, int NVC, int SPW>
 // Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
 __global__ void __launch_bounds__(64 * K1_WAVES, SPW == 2 ? 2 : SYSID_K1_MIN_WAVES_PER_EU)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
-                   int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp,
+                   int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
                    unsigned long long* __restrict__ work, double* __restrict__ dbg) {
   extern __shared__ double smem[];
   const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
@@ -485,8 +500,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   // Samples are handed out SPW at a time from a device counter (work[0]), so a workgroup that becomes
   // resident late, or a slow CU, only ever costs its own last samples.  The next ones are claimed one
   // step ahead and their inputs prefetched into registers (channel c -> lane c, c+HW, ...) while the
-  // current ones run.  The last wave to leave resets the counters for the next launch (work[1] counts
-  // departed waves; no wave touches work[0] after its last claim returned >= N).
+  // current ones run.  The counter lives in the launch's workspace and is zeroed on the launch stream
+  // right before the launch (host side), so no state carries over from one launch to the next.
   // The prefetch and the claim are issued at the top of a step and consumed in its middle (after the
   // projector): vmcnt retires in issue order, so consuming them at the top of the next step would first
   // wait for all of this step's panel stores.
@@ -1038,7 +1053,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
     // One G row (6 + 6*chain FMAs) feeds 42 FMAs.
-    double* out = panel + ((s + half) * nv) * ldp;
+    OutT* out = panel + ((s + half) * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
     auto block_row = [&](int r, const double* F, const int* dof, int cl, double* y) {
       const double* h = H1 + 6 * r;
@@ -1114,7 +1129,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const double2* s2 = reinterpret_cast<const double2*>(stg);
           for (int x = hl; x < n2; x += HW) {
             const int gg = x >= wy2 ? 1 : 0, c2 = x - gg * wy2;
-            panel_store(reinterpret_cast<double2*>(out + (int64_t)(gg * RH + rho) * ldp) + c2, s2[x]);
+            panel_store(out + (int64_t)(gg * RH + rho) * ldp + 2 * c2, s2[x].x, s2[x].y);
           }
         }
         wsync();
@@ -1126,13 +1141,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         double F[FBLK];
         int dof[MAXCH];  // the chain's dofs, read once: no dependent index load per row
         const int cl = block_setup(i, F, dof);
-        double* oi = out + 10 * (i - 1);
+        OutT* oi = out + 10 * (i - 1);
         for (int r = r0; r < r1; ++r) {
           double y[10];
           block_row(r, F, dof, cl, y);
-          double2* o2 = reinterpret_cast<double2*>(oi + (int64_t)r * ldp);
+          OutT* o2 = oi + (int64_t)r * ldp;
 #pragma unroll
-          for (int c = 0; c < 5; ++c) panel_store(o2 + c, make_double2(y[2 * c], y[2 * c + 1]));
+          for (int c = 0; c < 5; ++c) panel_store(o2 + 2 * c, y[2 * c], y[2 * c + 1]);
         }
       }
     }
@@ -1155,7 +1170,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const double fr = pr[jc] * sc;
           v2[u] = jj < 2 * nja ? fr : (kp.wy + jj == kp.w ? tps[r] : 0.0);  // pad: keep lines whole
         }
-        panel_store(reinterpret_cast<double2*>(out + (int64_t)r * ldp + kp.wy + 2 * m), make_double2(v2[0], v2[1]));
+        panel_store(out + (int64_t)r * ldp + kp.wy + 2 * m, v2[0], v2[1]);
       }
     }
 #if SYSID_PRIO
@@ -1169,13 +1184,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   if (lane == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + k, t_acc[k]);
 #endif
-  if (lane == 0) {
-    const unsigned long long total = (unsigned long long)gridDim.x * (blockDim.x >> 6);
-    if (atomicAdd(work + 1, 1ull) == total - 1) {
-      work[0] = 0;
-      work[1] = 0;
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1555,6 +1563,40 @@ k4_tau_error_final(const double* __restrict__ part, int nblocks, int nv, double*
     double sum = 0.0;
     for (int b = 0; b < nblocks; ++b) sum += part[(int64_t)b * nv + d];
     err_sq[d] = sum;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K5: the host entry point's de-interleave.  The panel's row r = [Y_proj | B_v | B_c | tau_proj | pad] is
+// split into the reference's separate stacked arrays (demo/spot_identification.py:84-87), each contiguous in
+// one device staging buffer, so every output leaves the device as ONE contiguous copy (instead of a 2-D copy
+// of rows x 8..1040 bytes).  One wave per row (grid-stride): the Y block as 16-byte pairs, the friction and
+// torque columns as 8-byte elements (nj may be odd).  A null output pointer skips that output.  HBM-bound.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k5_unstack(const double* __restrict__ panel, int64_t rows, int64_t ldp, int wy, int nj,
+           double* __restrict__ Y, double* __restrict__ tau, double* __restrict__ Bv, double* __restrict__ Bc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int y2 = wy >> 1, nf = 2 * nj + 1;
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const double* pr = panel + r * ldp;
+    if (Y != nullptr) {
+      const double2* src = reinterpret_cast<const double2*>(pr);
+      double2* dst = reinterpret_cast<double2*>(Y + r * wy);
+      for (int c = lane; c < y2; c += 64) dst[c] = src[c];
+    }
+    for (int c = lane; c < nf; c += 64) {
+      const double v = pr[wy + c];
+      if (c < nj) {
+        if (Bv != nullptr) Bv[r * nj + c] = v;
+      } else if (c < 2 * nj) {
+        if (Bc != nullptr) Bc[r * nj + (c - nj)] = v;
+      } else if (tau != nullptr) {
+        tau[r] = v;
+      }
+    }
   }
 }
 

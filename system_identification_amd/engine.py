@@ -256,11 +256,42 @@ class Engine:
             "ws": torch.empty(max(self.workspace_bytes(N, flags), 256), dtype=torch.uint8, device=dev),
         }
 
+    def _check_inputs(self, d_in, N: int):
+        """The C side cannot see tensor extents: a mismatched N would read other samples or fault, so the
+        shapes are checked here, before anything is enqueued."""
+        import torch
+        if d_in.dtype != torch.float64 or not d_in.is_cuda or d_in.dim() != 2 or d_in.shape[0] != self.in_rows:
+            raise ValueError(f"d_in must be a 2-D float64 CUDA tensor with {self.in_rows} channel rows")
+        if d_in.device.index != self.device:
+            raise ValueError(f"d_in is on {d_in.device}, the engine on cuda:{self.device}")
+        if d_in.stride(1) != 1 or (d_in.shape[0] > 1 and d_in.stride(0) < d_in.shape[1]):
+            raise ValueError("d_in must be channel-major with unit sample stride (a row-contiguous channel block)")
+        if not 0 <= int(N) <= d_in.shape[1]:
+            raise ValueError(f"N = {N} samples, but d_in holds {d_in.shape[1]}")
+
+    def _check_buffer(self, t, name: str, dtype, min_numel: int):
+        import torch
+        if not isinstance(t, torch.Tensor) or t.dtype != dtype or not t.is_cuda or t.device.index != self.device:
+            raise ValueError(f"{name} must be a {dtype} tensor on cuda:{self.device}")
+        if not t.is_contiguous() and not (t.dim() == 2 and t.stride(1) == 1):
+            raise ValueError(f"{name} must have unit stride along its last dimension")
+        if t.numel() < min_numel:
+            raise ValueError(f"{name} holds {t.numel()} elements, {min_numel} needed")
+
     def build_device(self, d_in, N: int, flags: int, bufs: dict, stream=None):
         """Stream-ordered launch on device tensors.  ``d_in`` is the (in_rows x ld) channel block."""
         import torch
-        if d_in.dtype != torch.float64 or not d_in.is_cuda or d_in.shape[0] != self.in_rows:
-            raise ValueError(f"d_in must be a float64 CUDA tensor with {self.in_rows} channel rows")
+        self._check_inputs(d_in, N)
+        P = bufs["panel"]
+        self._check_buffer(P, "panel", torch.float64, 0)
+        if P.dim() != 2 or P.stride(1) != 1 or P.shape[1] < self.panel_cols or P.shape[0] < int(N) * self.nv:
+            raise ValueError(f"panel must be a row-major (>= {int(N) * self.nv}) x (>= {self.panel_cols}) float64 "
+                             f"tensor, got {tuple(P.shape)} with strides {P.stride()}")
+        if flags & EMIT_GRAM:
+            self._check_buffer(bufs["gram"], "gram", torch.float64, self.panel_cols * self.panel_cols)
+            if not bufs["gram"].is_contiguous():
+                raise ValueError("gram must be contiguous")
+        self._check_buffer(bufs["ws"], "ws", torch.uint8, self.workspace_bytes(N, flags))
         ld = d_in.stride(0)
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.sysid_build_device(
@@ -286,8 +317,11 @@ class Engine:
         """Normal equations of N samples without materialising the N·nv-row panel (stream-ordered).
         precision: "f64" (parity), "f32" or "bf16" (MFMA in reduced precision, error reported)."""
         import torch
-        if d_in.dtype != torch.float64 or not d_in.is_cuda or d_in.shape[0] != self.in_rows:
-            raise ValueError(f"d_in must be a float64 CUDA tensor with {self.in_rows} channel rows")
+        self._check_inputs(d_in, N)
+        self._check_buffer(bufs["gram"], "gram", torch.float64, self.panel_cols * self.panel_cols)
+        if not bufs["gram"].is_contiguous():
+            raise ValueError("gram must be contiguous")
+        self._check_buffer(bufs["ws"], "ws", torch.uint8, self.gram_workspace_bytes(N))
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.sysid_build_gram_device(
             self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)), GRAM_PRECISION[precision],

@@ -71,14 +71,18 @@ class Solver():
             U, Sigma, VT = np.linalg.svd(self._Y, full_matrices=False)
             Sigma_inv = np.linalg.pinv(np.diag(Sigma))
             return VT.T @ Sigma_inv @ U.T @ self._tau
-        # same minimum-norm solution from the normal equations: x = pinv(G_YY) g_Y
+        # the minimum-norm solution from the normal equations, x = pinv(G_YY) g_Y.  The eigenvalues of the Gram
+        # carry an absolute error of about n eps w_max (the squaring loses what the SVD of Y keeps), so the
+        # rank cut is taken at that level (numpy's matrix_rank tolerance for G), not at the 1e-15 sigma_max
+        # of the stacked SVD: a smaller cut keeps the noise eigenvalues of the structurally unidentifiable
+        # parameter combinations and divides rounding noise of g by rounding noise of w.  The directions cut
+        # are those with sigma below sqrt(n eps) sigma_max (~2e-7 for Spot) — the noise floor of this form.
         n = self._nx
         G = self._gram["gram"][:n, :n]
         g = self._gram["Atb"][:n]
-        w, V = np.linalg.eigh(G)
-        # singular values of Y are sqrt(w); keep the numpy pinv cut (1e-15 sigma_max) on sigma
-        sig = np.sqrt(np.clip(w, 0.0, None))
-        keep = sig > 1e-15 * sig.max()
+        w, V = np.linalg.eigh(0.5 * (G + G.T))
+        wmax = float(w.max()) if w.size else 0.0
+        keep = w > max(wmax, 0.0) * n * np.finfo(np.float64).eps
         return V[:, keep] @ ((V[:, keep].T @ g) / w[keep])
 
     # ------------ Constrained Solver (LMI) ------------ #

@@ -102,11 +102,14 @@ class SystemIdentification(object):
 
     def _stacked_cached(self, q, dq, ddq, tau, cnt):
         """The demo calls get_projected_y_tau and then get_projected_friction_regressors on the same arrays;
-        one engine pass produces both, so the second call reuses it.  The cache key holds the identity,
-        shape and a checksum of every input, so arrays modified in between are recomputed."""
+        one engine pass produces both, so the second call reuses it.  The cache key holds the dtype, shape and
+        a content hash of every input, so an array modified in between (even keeping its sum, e.g. reordered
+        samples) is recomputed."""
+        import hashlib
+
         def fp(a):
-            a = np.asarray(a)
-            return (id(a), a.shape, float(np.sum(a, dtype=np.float64)))
+            a = np.ascontiguousarray(np.asarray(a))
+            return (a.dtype.str, a.shape, hashlib.blake2b(a.tobytes(), digest_size=16).hexdigest())
         key = tuple(fp(a) for a in (q, dq, ddq, cnt))
         tkey = fp(tau) if tau is not None else None
         if self._cache is not None and self._cache_key[0] == key and (tau is None or self._cache_key[1] == tkey):

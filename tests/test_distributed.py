@@ -76,3 +76,53 @@ def test_gloo_two_ranks_match_single_process(tmp_path):
     assert np.abs(got["gram"] - ref["gram"]).max() <= 1e-12 * np.abs(ref["gram"]).max()
     assert np.abs(got["Atb"] - ref["Atb"]).max() <= 1e-12 * np.abs(ref["Atb"]).max()
     assert abs(float(got["btb"]) - ref["btb"]) <= 1e-12 * ref["btb"]
+
+
+def _worker_uneven(rank, world, port, robot, splits, out_path):
+    """Each rank holds a shard of a DIFFERENT size (e.g. the tail rank of an uneven split) and exchanges the
+    packed (W+1)^2 buffer + row count through allreduce_normal_equations."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from oracle.ref_c import COracle
+    from system_identification_amd.distributed import allreduce_normal_equations
+    from system_identification_amd.model import load_robot
+    from system_identification_amd.synthetic import generate
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = load_robot(robot)
+    d = generate(m, splits[-1], config_index=5)
+    s0, s1 = splits[rank], splits[rank + 1]
+    o = COracle(m).build(*[d[k][:, s0:s1] for k in ("q", "dq", "ddq", "tau", "contact")], nthreads=1, stacked=False)
+    ne = {"gram": o["gram"], "Atb": o["Atb"], "btb": o["btb"], "num_rows": (s1 - s0) * m.nv}
+    out = allreduce_normal_equations(ne)
+    np.savez(out_path + f".{rank}.npz", **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_uneven_shards_allreduce(tmp_path):
+    import torch.multiprocessing as mp
+    from oracle.ref_c import COracle
+    from system_identification_amd.model import load_robot
+    from system_identification_amd.synthetic import generate
+    robot, splits = "spot", [0, 37, 260]  # 37 and 223 samples
+    out = str(tmp_path / "ne")
+    mp.start_processes(_worker_uneven, args=(2, _free_port(), robot, splits, out), nprocs=2, start_method="spawn")
+    m = load_robot(robot)
+    d = generate(m, splits[-1], config_index=5)
+    ref = COracle(m).build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], nthreads=1, stacked=False)
+    got = [dict(np.load(out + f".{r}.npz")) for r in range(2)]
+    for g in got:  # every rank holds the full normal equations, with the exact total row count
+        assert int(g["num_rows"]) == splits[-1] * m.nv
+        assert np.abs(g["gram"] - ref["gram"]).max() <= 1e-12 * np.abs(ref["gram"]).max()
+        assert np.abs(g["Atb"] - ref["Atb"]).max() <= 1e-12 * np.abs(ref["Atb"]).max()
+        assert abs(float(g["btb"]) - ref["btb"]) <= 1e-12 * ref["btb"]
+    assert np.array_equal(got[0]["gram"], got[1]["gram"])
+
+
+def test_row_count_survives_the_float_buffer():
+    """The row count rides in the all-reduced float64 buffer: exact for any count below 2^53."""
+    from system_identification_amd.distributed import pack_normal_equations
+    ne = {"gram": np.eye(3), "Atb": np.zeros(3), "btb": 0.0, "num_rows": 2 ** 40 + 12345}
+    buf, rows = pack_normal_equations(ne)
+    flat = np.concatenate([buf.reshape(-1), [float(rows)]])
+    assert int(round((flat + flat)[-1])) == 2 * (2 ** 40 + 12345)

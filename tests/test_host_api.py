@@ -102,3 +102,33 @@ def test_normal_equations_checkpoint_round_trip(tmp_path):
     back = load_normal_equations(tmp_path / "ne.npz")
     assert np.array_equal(back["gram"], ne["gram"]) and np.array_equal(back["Atb"], ne["Atb"])
     assert back["btb"] == 3.25 and back["num_rows"] == 40
+
+
+@pytest.mark.parametrize("robot", ["spot", "solo12"])
+def test_llsq_gram_path_on_real_panel(robot):
+    """the Gram-form llsq on a real projected regressor (oracle panel, 400 samples), whose columns
+    have structural rank deficiency (unidentifiable inertial combinations).  The minimum-norm solutions of the
+    stacked SVD (reference solver.py:32-39) and of the Gram must agree where the data identifies phi: the
+    predicted torques Y phi, and phi projected onto the right singular vectors with sigma > 1e-6 sigma_max."""
+    from oracle.ref_c import COracle
+    from system_identification_amd.model import load_robot
+    from system_identification_amd.synthetic import generate
+    model = load_robot(robot)
+    d = generate(model, 400, config_index=2)
+    out = COracle(model).build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], gram=False)
+    Y, t = out["Y_proj"], out["tau_proj"]
+    n = Y.shape[1]
+    nl = n // 10
+    phi_s = Solver(Y, t, nl, np.zeros(n), 1.0, None).solve_llsq_svd()
+    ne = {"gram": Y.T @ Y, "Atb": Y.T @ t, "btb": float(t @ t), "num_rows": Y.shape[0]}
+    phi_g = Solver.from_normal_equations(ne, nl, np.zeros(n), 1.0, None, friction=False).solve_llsq_svd()
+    assert np.all(np.isfinite(phi_g))
+    U, sig, VT = np.linalg.svd(Y, full_matrices=False)
+    assert sig[-1] < 1e-10 * sig[0]  # the panel really is rank deficient
+    ident = VT[sig > 1e-6 * sig[0]]
+    a, b = ident @ phi_s, ident @ phi_g
+    assert np.linalg.norm(a - b) <= 1e-6 * np.linalg.norm(a)
+    ps, pg = Y @ phi_s, Y @ phi_g
+    assert np.linalg.norm(ps - pg) <= 1e-6 * np.linalg.norm(ps)
+    # the Gram solution does not blow up along the unidentifiable directions
+    assert np.linalg.norm(phi_g) <= 1.5 * np.linalg.norm(phi_s)
