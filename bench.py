@@ -174,7 +174,7 @@ def main():
     eng = Engine(model, device=local)
     d_in = torch.from_numpy(channel_block(data)).cuda(local)
     flags = EMIT_ALL
-    tflags = EMIT_ALL | (GRAM_PRECISION[args.precision] if args.gram_only else 0)  # kernels timed below
+    tflags = EMIT_ALL | GRAM_PRECISION[args.precision]  # Gram-only kernels timed below
     stream = torch.cuda.current_stream(local)
 
     comm = None
@@ -239,19 +239,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only runs the
-    # same kernels chunk by chunk; they are timed on one chunk-sized batch.
+    # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only: the chunked
+    # path itself, each stage summed over its chunks.
     n_time = N
-    if args.gram_only:
-        n_time = min(N, max(4096, (512 << 20) // (model.nv * eng.panel_ld * 8)))
-        tb = eng.alloc_device(n_time, flags)
-        ms = eng.time_stages(d_in, n_time, tflags, tb, iters=max(5, args.steps))
-        del tb
-    else:
-        ms = eng.time_stages(d_in, N, flags, bufs, iters=max(5, args.steps))
+    ms = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
     nv, W = model.nv, eng.w
     in_b = (model.nq + 2 * nv + model.nj + model.n_ee) * 8
-    panel_b = nv * (W + 1) * 8
+    esize = {"f64": 8, "f32": 4, "bf16": 2}[args.precision] if args.gram_only else 8
+    panel_b = nv * (W + 1) * esize  # Gram-only at reduced precision: K1 writes the chunk panel in f32 / bf16
     bytes_k1 = in_b + panel_b                                                       # SURVEY §8d per sample
     flops_k2 = nv * W * (W + 1) + 2 * nv * W                                       # SYRK + Aᵀb per sample
     k1_gbs = n_time * bytes_k1 / (ms[0] * 1e-3) / 1e9

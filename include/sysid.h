@@ -130,6 +130,9 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
 /* Gram-only device entry point ("K1 fused with K2"): normal equations of N samples
  * without the N·nv-row panel.  The panel is produced in chunks of about 512 MiB inside the workspace
  * and folded into the same Gram accumulators chunk after chunk; d_gram as in sysid_build_device.
+ * flags may select a reduced-precision Gram (SYSID_GRAM_F32 / SYSID_GRAM_BF16, config 5): K1 then writes
+ * the chunk panel already rounded to f32 / bf16, and the Gram kernel runs on f32 / bf16 MFMA (f32
+ * accumulation per workgroup, f64 across workgroups).  The stacked-output entry points reject these flags.
  * Replaces what Solver.__init__ (src/solver.py:6-29) needs from the stacked arrays: G, g, bᵀb and
  * num_rows = N·nv (the objective scale of :190).  Stream-ordered, no allocation. */
 size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N);
@@ -177,9 +180,11 @@ int32_t sysid_dat_shape(const char* path, int64_t* rows, int64_t* cols);
 int32_t sysid_dat_read(const char* path, float* out, int64_t rows, int64_t cols, int32_t nthreads);
 const char* sysid_io_last_error(void);
 
-/* Kernel-only timing helper for bench.py: runs sysid_build_device `iters` times on the engine's
- * stream bracketed by HIP events and returns the mean milliseconds per kernel of each stage:
- * ms[0] = regressor/projector kernel, ms[1] = Gram kernel, ms[2] = Gram reduction kernel. */
+/* Kernel-only timing helper for bench.py: runs sysid_build_device (or, with d_panel == NULL, the Gram-only
+ * path of sysid_build_gram_device, workspace sized by sysid_gram_workspace_bytes) `iters` times on the
+ * engine's stream bracketed by HIP events and returns the mean milliseconds per step spent in each stage:
+ * ms[0] = regressor/projector kernel(s), ms[1] = Gram kernel(s), ms[2] = Gram reduction kernels.  The
+ * Gram-only path sums its chunks' K1 and K2 launches. */
 int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
                           double* d_panel, int64_t ld_panel, double* d_gram,
                           void* d_workspace, size_t workspace_bytes, int32_t iters, double* ms);

@@ -147,14 +147,39 @@ int k1_layout_hw(int variant) { return variant == K1_C4_NV18 ? 64 / k1_spw(varia
 
 const void* k1_fn(int variant) {
   switch (variant) {
-    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD>);
-    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN>);
-    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN>);
+    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, double>);
+    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, double>);
+    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, double>);
   }
 }
 
-int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
-              unsigned long long* work, hipStream_t st, double* dbg, int full = 0) {
+// Panel element of each Gram arithmetic: 0 = f64 (parity; every stacked output), 1 = f32, 2 = bf16 (the
+// Gram-only chunk panel of a reduced-precision Gram, rounded once by K1).
+size_t prec_bytes(int prec) { return prec == 0 ? 8 : prec == 1 ? 4 : 2; }
+
+// Gram arithmetic selected by the flags: 0 = f64 (parity), 1 = f32 MFMA, 2 = bf16 MFMA (error reported).
+int gram_prec(uint32_t flags) { return (flags & SYSID_GRAM_BF16) ? 2 : (flags & SYSID_GRAM_F32) ? 1 : 0; }
+
+template <typename OutT>
+void k1_launch_typed(sysid_engine* e, dim3 g1, dim3 b1, hipStream_t st, const K1Params& kp, const double* d_in,
+                     int64_t N, int64_t ld, OutT* d_panel, int64_t ld_panel, unsigned long long* work, double* dbg) {
+  switch (e->k1_variant) {
+    case K1_C4_NV18:
+      hipLaunchKernelGGL((k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, OutT>), g1, b1, e->k1_lds, st, kp,
+                         e->d_mimg, d_in, N, ld, d_panel, ld_panel, work, dbg);
+      break;
+    case K1_C4:
+      hipLaunchKernelGGL((k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in,
+                         N, ld, d_panel, ld_panel, work, dbg);
+      break;
+    default:
+      hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
+                         d_in, N, ld, d_panel, ld_panel, work, dbg);
+  }
+}
+
+int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
+              unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0) {
   K1Params kp = e->kp;
   HIP_TRY(e, hipMemsetAsync(work, 0, 2 * sizeof(unsigned long long), st));
   if (full) {
@@ -163,47 +188,40 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double
   }
   const int spw = k1_spw(e->k1_variant);
   kp.rg = k1_row_groups(kp.NJ, 64 / spw);
-  kp.out_cols = (int)std::min<int64_t>(ld_panel, e->ldp);
+  kp.out_cols = (int)std::min<int64_t>(ld_panel, prec == 0 ? e->ldp : ld_panel);
   const int64_t waves_needed = (N + spw - 1) / spw;
   const int64_t cap = (int64_t)e->cus * e->k1_blocks_per_cu;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + e->k1_waves - 1) / e->k1_waves));
   const dim3 g1((unsigned)grid), b1(64 * e->k1_waves);
-  switch (e->k1_variant) {
-    case K1_C4_NV18:
-      hipLaunchKernelGGL((k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N,
-                         ld, d_panel, ld_panel, work, dbg);
-      break;
-    case K1_C4:
-      hipLaunchKernelGGL((k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
-                         ld_panel, work, dbg);
-      break;
-    default:
-      hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
-                         ld_panel, work, dbg);
-  }
+  if (prec == 0)
+    k1_launch_typed(e, g1, b1, st, kp, d_in, N, ld, static_cast<double*>(d_panel), ld_panel, work, dbg);
+  else if (prec == 1)
+    k1_launch_typed(e, g1, b1, st, kp, d_in, N, ld, static_cast<float*>(d_panel), ld_panel, work, dbg);
+  else
+    k1_launch_typed(e, g1, b1, st, kp, d_in, N, ld, static_cast<__bf16*>(d_panel), ld_panel, work, dbg);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
 
-// Gram arithmetic selected by the flags: 0 = f64 (parity), 1 = f32 MFMA, 2 = bf16 MFMA (error reported).
-int gram_prec(uint32_t flags) { return (flags & SYSID_GRAM_BF16) ? 2 : (flags & SYSID_GRAM_F32) ? 1 : 0; }
-
-int launch_k2(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
+int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
               double* slab, hipStream_t st, int prec) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
   const dim3 g2(e->ngroups * ks), b2(64 * K2_WAVES);
+  const double* p64 = static_cast<const double*>(d_panel);
+  const float* p32 = static_cast<const float*>(d_panel);
+  const __bf16* p16 = static_cast<const __bf16*>(d_panel);
   switch (e->ntc) {
 #define SYSID_K2_CASE(NTC, KC)                                                                               \
   case NTC:                                                                                                 \
     if (prec == 0)                                                                                          \
-      hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles, \
+      hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, e->d_tiles,     \
                          e->ngroups, ks, e->nslots, accumulate, slab);                                      \
     else if (prec == 1)                                                                                     \
-      hipLaunchKernelGGL((k2_gram_syrk<float, NTC, KC>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles,  \
+      hipLaunchKernelGGL((k2_gram_syrk<float, NTC, KC>), g2, b2, 0, st, p32, rows, ld_panel, e->d_tiles,      \
                          e->ngroups, ks, e->nslots, accumulate, slab);                                      \
     else                                                                                                    \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, 32>), g2, b2, 0, st, d_panel, rows, ld_panel, e->d_tiles,    \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, 32>), g2, b2, 0, st, p16, rows, ld_panel, e->d_tiles,        \
                          e->ngroups, ks, e->nslots, accumulate, slab);                                      \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
@@ -247,6 +265,9 @@ int check_stages(sysid_engine* e, int64_t N, int64_t ld_panel, uint32_t flags, c
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0, need);
   if ((flags & SYSID_EMIT_GRAM) && ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
+  if (gram_prec(flags) != 0)
+    return set_err(e, SYSID_E_INVALID, "a reduced-precision Gram (SYSID_GRAM_F32/BF16) is a Gram-only mode "
+                   "(sysid_build_gram_device, or sysid_build without stacked outputs)");
   if (reinterpret_cast<uintptr_t>(d_ws) & 255)
     return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
   return SYSID_OK;
@@ -278,41 +299,88 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   return SYSID_OK;
 }
 
-// Gram-only: the panel never leaves the device and is produced chunk by chunk into the workspace
-// (about 512 MiB per chunk); K2 accumulates every chunk into the same slabs, K3 reduces once.
-int64_t gram_chunk(const sysid_engine* e, int64_t N) {
-  const int64_t per = (int64_t)e->nv * e->ldp * (int64_t)sizeof(double);
-  const int64_t c = std::max<int64_t>(4096, (512ll << 20) / per);
+// Gram-only: the panel never leaves the device and is produced chunk by chunk into the workspace; K2
+// accumulates every chunk into the same slabs, K3 reduces once.  The chunk panel is in the Gram's arithmetic
+// (f64, or f32 / bf16 rounded by K1) with ld a multiple of 16 bytes' worth of elements.
+size_t gram_chunk_bytes() {
+#ifdef SYSID_EXPERIMENTS
+  if (const char* v = std::getenv("SYSID_GRAM_CHUNK_MB")) return (size_t)std::max(1, std::atoi(v)) << 20;
+#endif
+  return (size_t)512 << 20;
+}
+
+int64_t gram_ld(const sysid_engine* e, int prec) {
+  const int64_t m = prec == 0 ? 2 : prec == 1 ? 4 : 8;
+  return (e->ncol + m - 1) / m * m;
+}
+
+int64_t gram_chunk(const sysid_engine* e, int64_t N, int prec) {
+  const int64_t per = (int64_t)e->nv * gram_ld(e, prec) * (int64_t)prec_bytes(prec);
+  const int64_t c = std::max<int64_t>(4096, (int64_t)gram_chunk_bytes() / per);
   return std::max<int64_t>(1, std::min(c, N));
 }
 
 // [K1 counter | panel chunk | K2 slabs | K3 partials]
-size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {
-  const int64_t rows = gram_chunk(e, N) * e->nv;
-  return WORK_BYTES + align256((size_t)rows * e->ldp * sizeof(double)) + slab_bytes(e, rows) + part_bytes(e, rows);
+size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
+  const int64_t rows = gram_chunk(e, N, prec) * e->nv;
+  return WORK_BYTES + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) + slab_bytes(e, rows) +
+         part_bytes(e, rows);
 }
 
+size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
+  return std::max({gram_ws_bytes_prec(e, N, 0), gram_ws_bytes_prec(e, N, 1), gram_ws_bytes_prec(e, N, 2)});
+}
+
+// ev (optional, diagnostics): 2 events per chunk + 2 for K3, recorded around each K1 / K2 / K3 launch.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
-                        void* d_ws, size_t ws_bytes, hipStream_t st) {
+                        void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr) {
   if (N <= 0) return SYSID_OK;
-  if (d_ws == nullptr || ws_bytes < gram_ws_bytes(e, N))
+  const int prec = gram_prec(flags);
+  if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
-                   gram_ws_bytes(e, N));
+                   gram_ws_bytes_prec(e, N, prec));
   if (reinterpret_cast<uintptr_t>(d_ws) & 255) return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
-  const int64_t C = gram_chunk(e, N), rows0 = C * e->nv;
+  const int64_t C = gram_chunk(e, N, prec), rows0 = C * e->nv, ldc = gram_ld(e, prec);
   auto* work = static_cast<unsigned long long*>(d_ws);
-  double* panel = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-  double* slab = reinterpret_cast<double*>(reinterpret_cast<char*>(panel) + align256((size_t)rows0 * e->ldp * sizeof(double)));
+  char* panel = static_cast<char*>(d_ws) + WORK_BYTES;
+  double* slab = reinterpret_cast<double*>(panel + align256((size_t)rows0 * ldc * prec_bytes(prec)));
   double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows0));
   const int ks0 = ksplit_for(e, rows0);
   int rc;
+  size_t k = 0;
+  auto mark = [&]() -> int {
+    if (ev && k < ev->size()) HIP_TRY(e, hipEventRecord((*ev)[k++], st));
+    return SYSID_OK;
+  };
   for (int64_t c0 = 0; c0 < N; c0 += C) {
     const int64_t n = std::min(C, N - c0);
-    if ((rc = launch_k1(e, d_in + c0, n, ld, panel, e->ldp, work, st, nullptr)) != SYSID_OK) return rc;
+    if ((rc = mark()) || (rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec)) || (rc = mark()))
+      return rc;
     const int ks = std::min(ks0, ksplit_for(e, n * e->nv));
-    if ((rc = launch_k2(e, panel, n * e->nv, e->ldp, ks, c0 > 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
+    if ((rc = launch_k2(e, panel, n * e->nv, ldc, ks, c0 > 0, slab, st, prec)) != SYSID_OK) return rc;
   }
-  return launch_k3(e, ks0, slab, part, d_gram, st);
+  if ((rc = mark())) return rc;
+  if ((rc = launch_k3(e, ks0, slab, part, d_gram, st))) return rc;
+  return mark();
+}
+
+int k4_blocks(const sysid_engine* e, int64_t N) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)e->cus * 4, N));
+}
+
+int launch_k4(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t N, const double* d_phi,
+              double* d_err_sq, void* d_ws, size_t ws_bytes, hipStream_t st) {
+  const int nb = k4_blocks(e, N);
+  if (d_ws == nullptr || ws_bytes < (size_t)nb * e->nv * sizeof(double))
+    return set_err(e, SYSID_E_INVALID, "workspace too small for the torque-error reduction");
+  if (e->wy > K4_MAXWY) return set_err(e, SYSID_E_MODEL, "regressor width %d > %d", e->wy, K4_MAXWY);
+  double* part = static_cast<double*>(d_ws);
+  hipLaunchKernelGGL(k4_tau_error, dim3((unsigned)nb), dim3(256), 0, st, d_panel, ld_panel, N, e->nv, e->wy, e->w,
+                     d_phi, part);
+  HIP_TRY(e, hipGetLastError());
+  hipLaunchKernelGGL(k4_tau_error_final, dim3(1), dim3(64), 0, st, part, nb, e->nv, d_err_sq);
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
 }
 
 // Host <-> device copies of the host entry points.  The caller's numpy arrays are pageable; a large copy
@@ -347,25 +415,6 @@ int launch_k5(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_p
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, (int64_t)e->cus * 8));
   hipLaunchKernelGGL(k5_unstack, dim3((unsigned)blocks), dim3(256), 0, st, d_panel, rows, ld_panel, e->wy, e->nj, Y,
                      tau, Bv, Bc);
-  HIP_TRY(e, hipGetLastError());
-  return SYSID_OK;
-}
-
-int k4_blocks(const sysid_engine* e, int64_t N) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)e->cus * 4, N));
-}
-
-int launch_k4(sysid_engine* e, const double* d_panel, int64_t ld_panel, int64_t N, const double* d_phi,
-              double* d_err_sq, void* d_ws, size_t ws_bytes, hipStream_t st) {
-  const int nb = k4_blocks(e, N);
-  if (d_ws == nullptr || ws_bytes < (size_t)nb * e->nv * sizeof(double))
-    return set_err(e, SYSID_E_INVALID, "workspace too small for the torque-error reduction");
-  if (e->wy > K4_MAXWY) return set_err(e, SYSID_E_MODEL, "regressor width %d > %d", e->wy, K4_MAXWY);
-  double* part = static_cast<double*>(d_ws);
-  hipLaunchKernelGGL(k4_tau_error, dim3((unsigned)nb), dim3(256), 0, st, d_panel, ld_panel, N, e->nv, e->wy, e->w,
-                     d_phi, part);
-  HIP_TRY(e, hipGetLastError());
-  hipLaunchKernelGGL(k4_tau_error_final, dim3(1), dim3(64), 0, st, part, nb, e->nv, d_err_sq);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
@@ -820,23 +869,47 @@ int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, con
 
 int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                           int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, int32_t iters, double* ms) {
-  if (!e || !ms || iters <= 0) return set_err(e, SYSID_E_INVALID, "bad arguments");
+  if (!e || !ms || iters <= 0 || N <= 0) return set_err(e, SYSID_E_INVALID, "bad arguments");
   HIP_TRY(e, hipSetDevice(e->device));
-  hipEvent_t ev[4];
-  for (auto& x : ev) HIP_TRY(e, hipEventCreate(&x));
   double acc[3] = {0, 0, 0};
   int rc = SYSID_OK;
-  for (int it = 0; it < iters && rc == SYSID_OK; ++it) {
-    rc = launch_stages(e, d_in, N, ld, flags, d_panel, ld_panel, d_gram, d_ws, ws_bytes, e->stream, ev);
-    if (rc != SYSID_OK) break;
-    if (hipEventSynchronize(ev[3]) != hipSuccess) { rc = set_err(e, SYSID_E_DEVICE, "event sync failed"); break; }
-    for (int k = 0; k < 3; ++k) {
-      float t = 0.f;
-      (void)hipEventElapsedTime(&t, ev[k], ev[k + 1]);
-      acc[k] += t;
+  if (d_panel == nullptr) {
+    // Gram-only path: per chunk K1 and K2, then K3; events around each launch
+    const int prec = gram_prec(flags);
+    const int64_t nchunks = (N + gram_chunk(e, N, prec) - 1) / gram_chunk(e, N, prec);
+    std::vector<hipEvent_t> ev((size_t)(2 * nchunks + 2));
+    for (auto& x : ev) HIP_TRY(e, hipEventCreate(&x));
+    for (int it = 0; it < iters && rc == SYSID_OK; ++it) {
+      rc = launch_gram_chunked(e, d_in, N, ld, flags, d_gram, d_ws, ws_bytes, e->stream, &ev);
+      if (rc != SYSID_OK) break;
+      if (hipEventSynchronize(ev.back()) != hipSuccess) { rc = set_err(e, SYSID_E_DEVICE, "event sync failed"); break; }
+      for (int64_t c = 0; c < nchunks; ++c) {
+        float t1 = 0.f, t2 = 0.f;
+        (void)hipEventElapsedTime(&t1, ev[2 * c], ev[2 * c + 1]);                        // K1 of chunk c
+        (void)hipEventElapsedTime(&t2, ev[2 * c + 1], ev[2 * c + 2]);                    // K2 of chunk c
+        acc[0] += t1;
+        acc[1] += t2;
+      }
+      float t3 = 0.f;
+      (void)hipEventElapsedTime(&t3, ev[2 * nchunks], ev[2 * nchunks + 1]);
+      acc[2] += t3;
     }
+    for (auto& x : ev) (void)hipEventDestroy(x);
+  } else {
+    hipEvent_t ev[4];
+    for (auto& x : ev) HIP_TRY(e, hipEventCreate(&x));
+    for (int it = 0; it < iters && rc == SYSID_OK; ++it) {
+      rc = launch_stages(e, d_in, N, ld, flags, d_panel, ld_panel, d_gram, d_ws, ws_bytes, e->stream, ev);
+      if (rc != SYSID_OK) break;
+      if (hipEventSynchronize(ev[3]) != hipSuccess) { rc = set_err(e, SYSID_E_DEVICE, "event sync failed"); break; }
+      for (int k = 0; k < 3; ++k) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, ev[k], ev[k + 1]);
+        acc[k] += t;
+      }
+    }
+    for (auto& x : ev) (void)hipEventDestroy(x);
   }
-  for (auto& x : ev) (void)hipEventDestroy(x);
   for (int k = 0; k < 3; ++k) ms[k] = acc[k] / iters;
   return rc;
 }

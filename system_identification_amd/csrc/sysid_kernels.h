@@ -1215,7 +1215,7 @@ __host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) /
 
 template <typename T, int NTC, int KC>
 __global__ void __launch_bounds__(64 * K2_WAVES)
-k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
              int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   typedef typename K2Acc<T>::type accT;
   constexpr int STRIDE = k2_stride(NTC);
@@ -1233,37 +1233,35 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
   // zero both buffers once: columns >= ldp (up to NTC*16) are never staged and must read as 0
   for (int x = threadIdx.x; x < 2 * BUF; x += NT) lds[x] = 0.0;
 
-  // staging slots: the chunk is KC*ldp contiguous doubles; thread slot u copies doubles [2x, 2x+1]
-  const int chunk_d2 = (int)((KC * ldp) / 2);            // ldp is even
-  constexpr int PER = (KC * NTC * 8 + NT - 1) / NT;       // >= ceil(KC*ldp/2 / NT)
+  // staging slots: the chunk is KC*ldp contiguous elements; thread slot u copies the 16 bytes [EP x, EP x + EP)
+  // (EP = 2 doubles or 4 floats; the panel's ld is a multiple of EP, so a slot never straddles two rows)
+  constexpr int EP = 16 / (int)sizeof(T);
+  const int chunk_s = (int)((KC * ldp) / EP);
+  constexpr int PER = (KC * NTC * 16 / EP + NT - 1) / NT;  // >= ceil(KC*ldp/EP / NT)
   int loff[PER];
   bool used[PER];
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int x = threadIdx.x + u * NT;
-    used[u] = x < chunk_d2;
-    const int e = 2 * x;
+    used[u] = x < chunk_s;
+    const int e = EP * x;
     const int row = used[u] ? e / (int)ldp : 0;
     loff[u] = used[u] ? row * STRIDE + (e - row * (int)ldp) : 0;
   }
-  double2 st[PER];
+  uint4 st[PER];
   auto load_chunk = [&](int64_t c0) {
-    const double2* src = reinterpret_cast<const double2*>(panel + c0 * ldp);
-    const int64_t lim = (r1 - c0) * ldp / 2;  // double2 slots inside [c0, r1)
+    const uint4* src = reinterpret_cast<const uint4*>(panel + c0 * ldp);
+    const int64_t lim = (r1 - c0) * ldp / EP;  // 16-byte slots inside [c0, r1)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int x = threadIdx.x + u * NT;
-      st[u] = (used[u] && x < lim) ? src[x] : double2{0.0, 0.0};
+      st[u] = (used[u] && x < lim) ? src[x] : make_uint4(0u, 0u, 0u, 0u);
     }
   };
   auto store_chunk = [&](T* b) {
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      if (used[u]) {
-        if constexpr (sizeof(T) == 8) *reinterpret_cast<double2*>(b + loff[u]) = st[u];
-        else *reinterpret_cast<float2*>(b + loff[u]) = make_float2((float)st[u].x, (float)st[u].y);
-      }
-    }
+    for (int u = 0; u < PER; ++u)
+      if (used[u]) *reinterpret_cast<uint4*>(b + loff[u]) = st[u];
   };
 
   // fragment columns of this wave: f = 4*s + {I0, I0+1, J0, J0+1} (16-column blocks)
@@ -1342,16 +1340,37 @@ k2_gram_syrk(const double* __restrict__ panel, int64_t rows, int64_t ldp, const 
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2 bf16: the same super-tile decomposition on v_mfma_f32_16x16x32_bf16.  A chunk of KC (a multiple of
-// 32) rows is staged column-major in LDS (column stride CS = KC + 8 bf16), so the fragment of lane l —
-// 8 consecutive rows 8(l>>4).. of column (l & 15) of a 16-column block, which is both the A layout
-// A[i = l&15][k = 8(l>>4) + j] and the B layout B[k][j = l&15] — is one 16-byte ds_read.  Staging item
-// = (column pair, 8-row group): eight 16-byte global loads, rounded f64 -> bf16 (RNE via f32), two
-// 16-byte LDS stores.  f32 accumulation per workgroup, f64 across workgroups (K3).
+// K2 bf16: the same super-tile decomposition on v_mfma_f32_16x16x32_bf16, from a bf16 panel (K1 rounds the
+// Gram-only chunk panel to bf16 as it writes it; ld a multiple of 8).  A chunk of KC (a multiple of 32) rows is
+// staged column-major in LDS (column stride CS = KC + 8 bf16), so the fragment of lane l — 8 consecutive rows
+// 8(l>>4).. of column (l & 15) of a 16-column block, which is both the A layout A[i = l&15][k = 8(l>>4) + j] and
+// the B layout B[k][j = l&15] — is one 16-byte ds_read.  Staging item = (8-column group, 8-row group): eight
+// 16-byte global loads (one row's 8 columns each), an 8x8 transpose of 16-bit elements in registers
+// (v_perm_b32), eight 16-byte LDS stores (one column's 8 rows each).  f32 accumulation per workgroup, f64
+// across workgroups (K3).
 // ------------------------------------------------------------------------------------------------
+// out[j] = column j of the 8x8 block whose row t is in[t] (8 bf16 per uint4, element j in the 16-bit half
+// (j & 1) of word (j >> 1)).
+__device__ __forceinline__ void transpose8x8_b16(const uint4 (&in)[8], uint4 (&out)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned sel = (j & 1) ? 0x07060302u : 0x05040100u;  // hi halves / lo halves of (b, a) -> a | b << 16
+    unsigned w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4& a = in[2 * q];
+      const uint4& b = in[2 * q + 1];
+      const unsigned wa = (j >> 1) == 0 ? a.x : (j >> 1) == 1 ? a.y : (j >> 1) == 2 ? a.z : a.w;
+      const unsigned wb = (j >> 1) == 0 ? b.x : (j >> 1) == 1 ? b.y : (j >> 1) == 2 ? b.z : b.w;
+      w[q] = __builtin_amdgcn_perm(wb, wa, sel);
+    }
+    out[j] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 template <int NTC, int KC>
 __global__ void __launch_bounds__(64 * K2_WAVES)
-k2_gram_syrk_bf16(const double* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
                   int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   static_assert(KC % 32 == 0, "bf16 K2 chunks are whole 32-row k-steps");
   constexpr int NCOL = NTC * 16;
@@ -1370,40 +1389,36 @@ k2_gram_syrk_bf16(const double* __restrict__ panel, int64_t rows, int64_t ldp, c
   // zero both buffers once: columns >= ldp are never staged and must read as 0
   for (int x = threadIdx.x; x < 2 * BUF; x += NT) lds[x] = (__bf16)0.0f;
 
-  const int npair = (int)(ldp >> 1);
-  constexpr int PER = (NTC * 8 * (KC / 8) + NT - 1) / NT;
-  int cp[PER], ro[PER];
+  const int ncg = (int)(ldp >> 3);  // 8-column groups per row
+  constexpr int PER = (NTC * 2 * (KC / 8) + NT - 1) / NT;
+  int cg[PER], ro[PER];
   bool used[PER];
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int it = threadIdx.x + u * NT;
-    used[u] = it < npair * (KC / 8);
-    ro[u] = used[u] ? it / npair : 0;
-    cp[u] = used[u] ? it - ro[u] * npair : 0;
+    used[u] = it < ncg * (KC / 8);
+    ro[u] = used[u] ? it / ncg : 0;
+    cg[u] = used[u] ? it - ro[u] * ncg : 0;
   }
-  double2 st[PER][8];
+  uint4 st[PER][8];
   auto load_chunk = [&](int64_t c0) {
 #pragma unroll
     for (int u = 0; u < PER; ++u)
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int64_t r = c0 + 8 * ro[u] + t;
-        st[u][t] = (used[u] && r < r1) ? reinterpret_cast<const double2*>(panel + r * ldp)[cp[u]]
-                                       : double2{0.0, 0.0};
+        st[u][t] = (used[u] && r < r1) ? reinterpret_cast<const uint4*>(panel + r * ldp)[cg[u]]
+                                       : make_uint4(0u, 0u, 0u, 0u);
       }
   };
   auto store_chunk = [&](__bf16* b) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       if (!used[u]) continue;
-      bf16x8 lo, hi;
+      uint4 col[8];
+      transpose8x8_b16(st[u], col);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        lo[t] = (__bf16)(float)st[u][t].x;
-        hi[t] = (__bf16)(float)st[u][t].y;
-      }
-      *reinterpret_cast<bf16x8*>(b + (2 * cp[u]) * CS + 8 * ro[u]) = lo;
-      *reinterpret_cast<bf16x8*>(b + (2 * cp[u] + 1) * CS + 8 * ro[u]) = hi;
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<uint4*>(b + (8 * cg[u] + j) * CS + 8 * ro[u]) = col[j];
     }
   };
 

@@ -330,11 +330,15 @@ class Engine:
         self._check(rc)
 
     def time_stages(self, d_in, N: int, flags: int, bufs: dict, iters: int = 10) -> list:
-        """Mean ms per kernel [regressor/projector, Gram SYRK, Gram reduce] (HIP events)."""
+        """Mean ms per step in each stage [regressor/projector, Gram SYRK, Gram reduce] (HIP events).  With
+        Gram-only buffers (alloc_gram_device: no "panel") the chunked Gram-only path is timed, its chunks summed."""
+        self._check_inputs(d_in, N)
         ms = np.zeros(3)
+        panel = bufs.get("panel")
         rc = self.lib.sysid_time_stages(
             self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)), int(flags),
-            ctypes.c_void_p(bufs["panel"].data_ptr()), int(bufs["panel"].stride(0)),
+            ctypes.c_void_p(panel.data_ptr() if panel is not None else None),
+            int(panel.stride(0)) if panel is not None else 0,
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), int(iters), _ptr(ms))
         self._check(rc)
