@@ -856,14 +856,22 @@ int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, con
     r0 += nrows[k];
   }
   if ((rc = launch_k1(e, e->d_in, N, N, e->d_panel, e->ldp, e->d_work, st, nullptr, 1)) != SYSID_OK) return rc;
-  const size_t pitch = (size_t)e->ldp * sizeof(double);
-  if (Y)
-    HIP_TRY(e, hipMemcpy2DAsync(Y, (size_t)e->wy * sizeof(double), e->d_panel, pitch, (size_t)e->wy * sizeof(double),
-                                rows, hipMemcpyDeviceToHost, st));
-  if (F)
-    HIP_TRY(e, hipMemcpy2DAsync(F, sizeof(double), e->d_panel + e->w, pitch, sizeof(double), rows,
-                                hipMemcpyDeviceToHost, st));
-  HIP_TRY(e, hipStreamSynchronize(st));
+  // de-interleave on the device (Y block, and the torque column that holds F), one contiguous copy each
+  const size_t nY = Y ? (size_t)rows * e->wy : 0, nF = F ? (size_t)rows : 0;
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_out), &e->out_cap, (nY + nF) * sizeof(double) + 64))) return rc;
+  if ((rc = launch_k5(e, e->d_panel, rows, e->ldp, Y ? e->d_out : nullptr, F ? e->d_out + nY : nullptr, nullptr,
+                      nullptr, st)) != SYSID_OK)
+    return rc;
+  std::vector<void*> reg;
+  if ((Y && (rc = host_copy(e, Y, e->d_out, nY * sizeof(double), hipMemcpyDeviceToHost, st, &reg))) ||
+      (F && (rc = host_copy(e, F, e->d_out + nY, nF * sizeof(double), hipMemcpyDeviceToHost, st, &reg)))) {
+    (void)hipStreamSynchronize(st);
+    host_unregister(e, reg);
+    return rc;
+  }
+  const hipError_t sst = hipStreamSynchronize(st);
+  host_unregister(e, reg);
+  if (sst != hipSuccess) return set_err(e, SYSID_E_DEVICE, "stream sync failed: %s", hipGetErrorString(sst));
   return SYSID_OK;
 }
 

@@ -551,7 +551,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   }
   int64_t s1 = s < N ? claim_value(claim_issue()) : N;
 #ifdef SYSID_STAMPS
-  unsigned long long t_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -1105,6 +1105,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // store per lane per 512 contiguous bytes instead of 16-byte pieces 80 bytes apart.
     // (The host picks this kernel only for 11..16 bodies: rg = 2 row groups, nyi <= 32 lanes, and the two
     // staged rows fit in the joint records.)
+#ifndef SYSID_K1_COLV
+#define SYSID_K1_COLV 2
+#endif
     if constexpr (SYSID_STAGE_Y && NVC == 18 && HW == 32) {
       constexpr int RH = NVC / 2;  // rows per row group
       const bool act = hl < nyi && valid;
@@ -1112,6 +1115,29 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       double F[FBLK];
       int dof[MAXCH];
       const int cl = block_setup(i, F, dof);
+#if SYSID_K1_COLV >= 2
+      // The chain's motion axes are the same for every row: read once into registers (masked past the
+      // chain), and each row's H1 / P entries are loaded one row ahead, so a row's LDS reads are in flight
+      // while the previous row is multiplied and staged.
+      double jw[MAXCH][6];
+#pragma unroll
+      for (int t = 0; t < MAXCH; ++t)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) jw[t][k] = t < cl ? Jws[6 * dof[t] + k] : 0.0;
+      double hn[6], pn[MAXCH];
+      auto row_load = [&](int r, double* h, double* pp) {
+        const double2* h2 = reinterpret_cast<const double2*>(H1 + 6 * r);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const double2 v = h2[k];
+          h[2 * k] = v.x;
+          h[2 * k + 1] = v.y;
+        }
+#pragma unroll
+        for (int t = 0; t < MAXCH; ++t) pp[t] = Ps[r * NVC + dof[t]];
+      };
+      row_load(g * RH, hn, pn);
+#endif
       wsync();  // every read of the joint records precedes the first staging store
       double* stg = body;  // [row group][wy]
       const int wy2 = kp.wy >> 1, n2 = kp.rg * wy2;
@@ -1119,7 +1145,32 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       for (int rho = 0; rho < RH; ++rho) {
         if (act) {
           double y[10];
+#if defined(SYSID_EXP_NO_YCOMP)
+#pragma unroll
+          for (int c = 0; c < 10; ++c) y[c] = F[c];  // diagnostics build: no row products
+#elif SYSID_K1_COLV >= 2
+          double G[6], pc[MAXCH];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) G[k] = hn[k];
+#pragma unroll
+          for (int t = 0; t < MAXCH; ++t) pc[t] = pn[t];
+          if (rho + 1 < RH) row_load(g * RH + rho + 1, hn, pn);
+#pragma unroll
+          for (int t = 0; t < MAXCH; ++t) {
+            const double pv = t < cl ? pc[t] : 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) G[k] += pv * jw[t][k];
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            y[c] = G[0] * F[6 * c] + G[1] * F[6 * c + 1] + G[2] * F[6 * c + 2] + G[3] * F[6 * c + 3] +
+                   G[4] * F[6 * c + 4] + G[5] * F[6 * c + 5];
+#pragma unroll
+          for (int c = 0; c < 6; ++c)
+            y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
+#else
           block_row(g * RH + rho, F, dof, cl, y);
+#endif
           double2* sp = reinterpret_cast<double2*>(stg + g * kp.wy + 10 * (i - 1));
 #pragma unroll
           for (int c = 0; c < 5; ++c) sp[c] = make_double2(y[2 * c], y[2 * c + 1]);
@@ -1129,7 +1180,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const double2* s2 = reinterpret_cast<const double2*>(stg);
           for (int x = hl; x < n2; x += HW) {
             const int gg = x >= wy2 ? 1 : 0, c2 = x - gg * wy2;
+#ifndef SYSID_EXP_NO_YSTORE
             panel_store(out + (int64_t)(gg * RH + rho) * ldp + 2 * c2, s2[x].x, s2[x].y);
+#else
+            if (s2[x].x == 1.2345e300) panel_store(out, s2[x].x, s2[x].y);  // diagnostics build: keep the reads
+#endif
           }
         }
         wsync();
@@ -1152,6 +1207,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
     }
 
+    K1_STAMP(8)
     // ---- [B_v | B_c | tau_proj | pad]: lane = (row, column pair), 16-byte stores ----
     {
       const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
@@ -1170,7 +1226,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const double fr = pr[jc] * sc;
           v2[u] = jj < 2 * nja ? fr : (kp.wy + jj == kp.w ? tps[r] : 0.0);  // pad: keep lines whole
         }
+#ifndef SYSID_EXP_NO_FSTORE
         panel_store(out + (int64_t)r * ldp + kp.wy + 2 * m, v2[0], v2[1]);
+#else
+        if (v2[0] == 1.2345e300) panel_store(out, v2[0], v2[1]);  // diagnostics build
+#endif
       }
     }
 #if SYSID_PRIO
@@ -1182,7 +1242,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   }
 #ifdef SYSID_STAMPS
   if (lane == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + k, t_acc[k]);
+    for (int k = 0; k < 9; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + k, t_acc[k]);
 #endif
 }
 

@@ -15,7 +15,7 @@ out = np.zeros(16, dtype=np.uint64)
 for it in range(2):
     out[:] = 0
     lib.sysid_debug_stamps(eng._h, ctypes.c_void_p(din.data_ptr()), N, din.stride(0), ctypes.c_void_p(bufs["panel"].data_ptr()), bufs["panel"].stride(0), out.ctypes.data)
-names = ["in", "fk", "axes", "Jc+norms", "mgs", "P", "H1+tp", "cols"]
-tot = out[:8].sum()
+names = ["in", "fk", "axes", "Jc+norms", "mgs", "P", "H1+tp", "fric", "Ycols"]
+tot = out[:9].sum()
 for k, n in enumerate(names): print("%6s %10.0f cycles/sample  %5.1f%%" % (n, out[k] / N, 100 * out[k] / tot))
 print("total %.0f cycles per sample per workgroup" % (tot / N))
