@@ -177,15 +177,27 @@ def main():
     tflags = EMIT_ALL | GRAM_PRECISION[args.precision]  # Gram-only kernels timed below
     stream = torch.cuda.current_stream(local)
 
-    comm = None
+    comm, exchange_name = None, None
     if world > 1:
         # the engine's own exchange step (C ABI: sysid_rccl_unique_id / _comm_init / sysid_allreduce_gram); the
-        # 128-byte RCCL id travels from rank 0 over the torch process group
+        # 128-byte RCCL id travels from rank 0 over the torch process group.  Should the C-ABI communicator fail
+        # to come up on some node, the same all-reduce runs through torch.distributed (RCCL) and the JSON says so.
         def share_id(raw):
             box = [raw if rank == 0 else None]
             dist.broadcast_object_list(box, src=0)
             return box[0]
-        comm = RcclGramComm(eng, rank, world, share_id=share_id)
+        try:
+            comm = RcclGramComm(eng, rank, world, share_id=share_id)
+            ok = torch.tensor([1], dtype=torch.int32, device="cuda")
+        except Exception as exc:  # noqa: BLE001 - reported in the JSON line
+            comm, exchange_name = None, f"torch.distributed.all_reduce (C-ABI RCCL init failed: {exc})"
+            ok = torch.tensor([0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same path
+        if int(ok.item()) == 0 and comm is not None:
+            comm.close()
+            comm, exchange_name = None, "torch.distributed.all_reduce (C-ABI RCCL init failed on another rank)"
+        if comm is not None:
+            exchange_name = "sysid_allreduce_gram (RCCL, C ABI)"
 
     if args.gram_only:
         bufs = eng.alloc_gram_device(N)
@@ -201,6 +213,8 @@ def main():
     def exchange():
         if comm is not None:
             comm.allreduce_gram(bufs["gram"], stream=stream.cuda_stream)
+        elif world > 1:
+            dist.all_reduce(bufs["gram"])
 
     # One step's launches (memsets + K1 + K2 + K3) captured once into a HIP graph and replayed: the same
     # kernels over the same buffers, without the per-launch host gaps.  The RCCL all-reduce stays eager.
@@ -286,7 +300,7 @@ def main():
                        "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
                    "robot": args.robot, "samples_per_gpu": N, "total_samples_per_step": total_per_step,
                    "nv": nv, "W": W, "parallelism": f"dp{world}",
-                   "exchange": "sysid_allreduce_gram (RCCL, C ABI)" if world > 1 else None},
+                   "exchange": exchange_name},
         "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
         "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},

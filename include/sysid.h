@@ -128,7 +128,7 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
                            void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Gram-only device entry point ("K1 fused with K2"): normal equations of N samples
- * without the N·nv-row panel.  The panel is produced in chunks of about 512 MiB inside the workspace
+ * without the N·nv-row panel.  The panel is produced in chunks of about 1 GiB inside the workspace
  * and folded into the same Gram accumulators chunk after chunk; d_gram as in sysid_build_device.
  * flags may select a reduced-precision Gram (SYSID_GRAM_F32 / SYSID_GRAM_BF16, config 5): K1 then writes
  * the chunk panel already rounded to f32 / bf16, and the Gram kernel runs on f32 / bf16 MFMA (f32

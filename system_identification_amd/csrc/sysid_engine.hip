@@ -90,8 +90,9 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 
 // K2 split-K: one workgroup per CU and super-tile group; wide Grams (>= 16 tile columns, small row
 // chunks) run two workgroups per CU (measured: G1 K2 -11%, Spot unchanged net of the larger K3).
-int ksplit_for(const sysid_engine* e, int64_t rows) {
-  const int mult = e->ntc >= 16 ? 2 : 1;
+int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
+  // the bf16 kernel's large chunks take most of a CU's LDS: one workgroup per CU
+  const int mult = e->ntc >= 16 && prec != 2 ? 2 : 1;
   int ks = std::max(1, mult * e->cus / std::max(1, e->ngroups));
   const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
@@ -217,12 +218,12 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
     if (prec == 0)                                                                                          \
       hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, e->d_tiles,     \
                          e->ngroups, ks, e->nslots, accumulate, slab);                                      \
-    else if (prec == 1)                                                                                     \
-      hipLaunchKernelGGL((k2_gram_syrk<float, NTC, KC>), g2, b2, 0, st, p32, rows, ld_panel, e->d_tiles,      \
+    else if (prec == 1) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                    \
+      hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, e->d_tiles,  \
                          e->ngroups, ks, e->nslots, accumulate, slab);                                      \
     else                                                                                                    \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, 32>), g2, b2, 0, st, p16, rows, ld_panel, e->d_tiles,        \
-                         e->ngroups, ks, e->nslots, accumulate, slab);                                      \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, b2, 0, st, p16, rows, ld_panel,       \
+                         e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                          \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
     SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
@@ -302,11 +303,14 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
 // Gram-only: the panel never leaves the device and is produced chunk by chunk into the workspace; K2
 // accumulates every chunk into the same slabs, K3 reduces once.  The chunk panel is in the Gram's arithmetic
 // (f64, or f32 / bf16 rounded by K1) with ld a multiple of 16 bytes' worth of elements.
+// Chunk panel of ~1 GiB: every K1 launch ends in a tail of partly idle CUs (a G1 wave-step is ~20 us), so few
+// large chunks beat MALL-sized ones (G1 125k bf16 step: 64 MB chunks 11.2 ms, 128 MB 10.3, 256 MB 9.3,
+// 512 MB 8.6, 1 GiB 8.3; profiles/r02_p2).
 size_t gram_chunk_bytes() {
 #ifdef SYSID_EXPERIMENTS
   if (const char* v = std::getenv("SYSID_GRAM_CHUNK_MB")) return (size_t)std::max(1, std::atoi(v)) << 20;
 #endif
-  return (size_t)512 << 20;
+  return (size_t)1 << 30;
 }
 
 int64_t gram_ld(const sysid_engine* e, int prec) {
@@ -345,7 +349,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   char* panel = static_cast<char*>(d_ws) + WORK_BYTES;
   double* slab = reinterpret_cast<double*>(panel + align256((size_t)rows0 * ldc * prec_bytes(prec)));
   double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows0));
-  const int ks0 = ksplit_for(e, rows0);
+  const int ks0 = ksplit_for(e, rows0, prec);  // <= ksplit_for(e, rows0): the slabs fit the workspace
   int rc;
   size_t k = 0;
   auto mark = [&]() -> int {
@@ -356,7 +360,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     const int64_t n = std::min(C, N - c0);
     if ((rc = mark()) || (rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec)) || (rc = mark()))
       return rc;
-    const int ks = std::min(ks0, ksplit_for(e, n * e->nv));
+    const int ks = std::min(ks0, ksplit_for(e, n * e->nv, prec));
     if ((rc = launch_k2(e, panel, n * e->nv, ldc, ks, c0 > 0, slab, st, prec)) != SYSID_OK) return rc;
   }
   if ((rc = mark())) return rc;

@@ -1263,6 +1263,12 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef float flt4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int K2_SPW = 2;   // super-tiles per wave
+#ifndef SYSID_K2_UNIFORM
+#define SYSID_K2_UNIFORM 0  // readfirstlane'd descriptors measured slower (G1 K2 1.80 -> 2.26 ms, Spot +3%)
+#endif
+#ifndef SYSID_K2_ALLTILES
+#define SYSID_K2_ALLTILES 0  // computing the redundant tiles too measured slower (Spot +6%, G1 +9%)
+#endif
 
 // Reduced-precision Gram (error reported, not gated): T = float runs the same
 // kernel on v_mfma_f32_16x16x4_f32 (panel rounded to f32 while staged, f32 accumulation per workgroup,
@@ -1272,6 +1278,16 @@ template <> struct K2Acc<double> { typedef dbl4 type; };
 template <> struct K2Acc<float> { typedef flt4 type; };
 
 __host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) / 32) * 32 + 16; }
+
+// Rows per staged chunk of the bf16 kernel: as many whole 32-row k-steps as two column-major LDS buffers of
+// NTC*16 columns x (KC + 8) bf16 fit in ~150 KB, at most 128.  Each chunk is one global-load latency of the
+// staging loop, and one bf16 k-step is only 16 cycles of MFMA per tile: small chunks left the kernel
+// latency-bound (KC = 32: G1 125k K2 4.4 ms, 0.7 TB/s of staged panel).
+__host__ __device__ constexpr int k2_bf16_kc(int ntc) {
+  return ((150 * 1024 / (64 * ntc)) - 8) / 32 * 32 > 128 ? 128
+         : ((150 * 1024 / (64 * ntc)) - 8) / 32 * 32 < 32 ? 32
+                                                          : ((150 * 1024 / (64 * ntc)) - 8) / 32 * 32;
+}
 
 template <typename T, int NTC, int KC>
 __global__ void __launch_bounds__(64 * K2_WAVES)
@@ -1315,7 +1331,11 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int x = threadIdx.x + u * NT;
+#ifndef SYSID_EXP_K2_NOLOAD
       st[u] = (used[u] && x < lim) ? src[x] : make_uint4(0u, 0u, 0u, 0u);
+#else
+      st[u] = make_uint4((unsigned)x, 1u, 2u, 3u);  // diagnostics build: no global loads
+#endif
     }
   };
   auto store_chunk = [&](T* b) {
@@ -1330,7 +1350,13 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   bool need[K2_SPW][4];  // wave-uniform: skip the lower tile of a diagonal super-tile, tiles past NTC
 #pragma unroll
   for (int s = 0; s < K2_SPW; ++s) {
-    const int2 sp = supers[sbase + s];
+    int2 sp = supers[sbase + s];
+#if SYSID_K2_UNIFORM
+    // wave-uniform by construction (sbase depends on the wave only): SGPRs, so the tile tests below are
+    // scalar branches instead of exec-masked blocks around every MFMA
+    sp.x = __builtin_amdgcn_readfirstlane(sp.x);
+    sp.y = __builtin_amdgcn_readfirstlane(sp.y);
+#endif
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1370,7 +1396,11 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
         constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
+#if SYSID_K2_ALLTILES
+          if (!live[s]) continue;  // every tile of a live super-tile: the redundant ones land in unused slots
+#else
           if (!need[s][t]) continue;
+#endif
           if constexpr (sizeof(T) == 8)
             acc[s][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
           else
@@ -1487,7 +1517,13 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
   bool need[K2_SPW][4];
 #pragma unroll
   for (int s = 0; s < K2_SPW; ++s) {
-    const int2 sp = supers[sbase + s];
+    int2 sp = supers[sbase + s];
+#if SYSID_K2_UNIFORM
+    // wave-uniform by construction (sbase depends on the wave only): SGPRs, so the tile tests below are
+    // scalar branches instead of exec-masked blocks around every MFMA
+    sp.x = __builtin_amdgcn_readfirstlane(sp.x);
+    sp.y = __builtin_amdgcn_readfirstlane(sp.y);
+#endif
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {

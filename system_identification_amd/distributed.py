@@ -84,12 +84,19 @@ class RcclGramComm:
         import ctypes
         self.lib, self.engine = engine.lib, engine
         uid = ctypes.create_string_buffer(128)
+        err = None
         if rank == 0 and self.lib.sysid_rccl_unique_id(uid) != 0:
-            raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
+            err = self.lib.sysid_rccl_last_error().decode()
         if world > 1:
             if share_id is None:
                 raise ValueError("world > 1 needs share_id to distribute the RCCL unique id")
-            uid = ctypes.create_string_buffer(bytes(share_id(uid.raw)), 128)
+            # rank 0 shares an empty id when it has none, so that no rank is left waiting in comm_init
+            got = bytes(share_id(b"" if err else uid.raw))
+            if len(got) != 128:
+                raise RuntimeError(err or "rank 0 could not create an RCCL unique id")
+            uid = ctypes.create_string_buffer(got, 128)
+        if err:
+            raise RuntimeError(err)
         self._comm = ctypes.c_void_p()
         if self.lib.sysid_rccl_comm_init(ctypes.byref(self._comm), int(world), uid, int(rank), int(engine.device)) != 0:
             raise RuntimeError(self.lib.sysid_rccl_last_error().decode())

@@ -250,7 +250,7 @@ def test_hip_graph_replay_matches_eager(robot, N):
 
 @pytest.mark.parametrize("robot,N", [("spot", 50000), ("g1_29dof", 12000)])
 def test_gram_only_chunked(robot, N):
-    """Gram-only path (panel produced in ~512 MiB chunks on the device, several chunks here) against
+    """Gram-only path (panel produced in ~1 GiB chunks on the device, several chunks here) against
     the full-panel path, on the host API and on the device API; bitwise repeatable."""
     import torch
     model = load_robot(robot)
