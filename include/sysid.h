@@ -26,9 +26,9 @@
  *   - A handle is bound to one device and owns one HIP stream.  The host-buffer entry points (sysid_build,
  *     sysid_build_full, sysid_tau_error) use buffers owned by the handle: they are synchronous and not
  *     re-entrant (one thread at a time per handle).  The device entry points keep every piece of per-launch
- *     state in the caller's workspace (K1's sample counter is its first 256 bytes, zeroed on the launch
- *     stream before each launch): launches of one handle on different streams with different workspaces may
- *     run concurrently, and an aborted launch leaves nothing behind for the next one.
+ *     state in the caller's workspace (K1's sample counters, one per XCD shard of the samples, are its first
+ *     1 KiB, zeroed on the launch stream before each launch): launches of one handle on different streams with
+ *     different workspaces may run concurrently, and an aborted launch leaves nothing behind for the next one.
  *   - Every argument check of an entry point happens before its first enqueue: an error return means that
  *     nothing was enqueued (also under graph capture).
  *

@@ -35,7 +35,7 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // Every device workspace starts with K1's sample counter (one 256-byte piece).  It is zeroed on the launch
 // stream right before each K1 launch, so launches are independent of each other: an aborted launch leaves
 // nothing behind, and launches on different streams with different workspaces may run concurrently.
-constexpr size_t WORK_BYTES = 256;
+constexpr size_t WORK_BYTES = 128 * K1_SHARDS;  // one 128-byte line per claim counter
 
 }  // namespace
 
@@ -182,7 +182,7 @@ void k1_launch_typed(sysid_engine* e, dim3 g1, dim3 b1, hipStream_t st, const K1
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
               unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0) {
   K1Params kp = e->kp;
-  HIP_TRY(e, hipMemsetAsync(work, 0, 2 * sizeof(unsigned long long), st));
+  HIP_TRY(e, hipMemsetAsync(work, 0, WORK_BYTES, st));
   if (full) {
     kp.full = 1;
     kp.in_rows = e->in_lds;
@@ -631,8 +631,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
-  if (st == hipSuccess) st = hipMalloc(&e->d_work, 2 * sizeof(unsigned long long));
-  if (st == hipSuccess) st = hipMemset(e->d_work, 0, 2 * sizeof(unsigned long long));
+  if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
+  if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   if (st == hipSuccess) st = hipMalloc(&e->d_tiles, both.size() * sizeof(int2));
   if (st == hipSuccess) st = hipMemcpy(e->d_tiles, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice);
   // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget

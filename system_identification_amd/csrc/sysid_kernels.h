@@ -20,6 +20,7 @@ constexpr int JT_FREEFLYER = 1;
 constexpr int JT_REVOLUTE = 2;
 constexpr int K1_WAVES = 4;            // waves (= samples in flight) per K1 workgroup
 constexpr int K2_WAVES = 8;            // waves per K2 workgroup
+constexpr int K1_SHARDS = 8;           // K1 sample ranges / claim counters (one per XCD), 128 B apart
 
 // ------------------------------------------------------------------------------------------------
 // layouts shared by host and device
@@ -438,6 +439,9 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 // SPW: samples per wave (1 or 2).  With SPW > 1 each 64/SPW-lane slice of the wave carries its own
 // sample through every phase, so the lane-starved serial phases (forward pass, Gram-Schmidt steps) do SPW
 // samples per instruction; each slice has its own LDS region.
+#ifndef SYSID_EXP_SKIP
+#define SYSID_EXP_SKIP 0  // diagnostics builds only: bit mask of K1 phases to skip (timing attribution)
+#endif
 template <int MAXCH, int NVC, int SPW, typename OutT>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
@@ -497,29 +501,56 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   double* tps = wr + L.tp;
   double* dqs = wr + L.dqs;
 
-  // Samples are handed out SPW at a time from a device counter (work[0]), so a workgroup that becomes
-  // resident late, or a slow CU, only ever costs its own last samples.  The next ones are claimed one
-  // step ahead and their inputs prefetched into registers (channel c -> lane c, c+HW, ...) while the
-  // current ones run.  The counter lives in the launch's workspace and is zeroed on the launch stream
-  // right before the launch (host side), so no state carries over from one launch to the next.
+  // Samples are handed out SPW at a time from device counters, so a workgroup that becomes resident late,
+  // or a slow CU, only ever costs its own last samples.  The next ones are claimed one step ahead and their
+  // inputs prefetched into registers (channel c -> lane c, c+HW, ...) while the current ones run.  The
+  // counters live in the launch's workspace and are zeroed on the launch stream right before the launch
+  // (host side), so no state carries over from one launch to the next.
+  // Sharded: one returning atomic on a single word serialises at ~88 per microsecond chip-wide (Spot 20k
+  // = 10,000 claims ~ 114 us: most of K1's time; measured with every phase compiled out, 0.155 of 0.236 ms).
+  // The samples are split into K1_SHARDS contiguous ranges with a counter each (128 B apart); a wave claims
+  // from the range of its own XCD first (HW_REG_XCC_ID: speed only, never correctness), then from the others
+  // in turn, skipping an exhausted range after one plain (relaxed, agent-scope) read of its counter.
   // The prefetch and the claim are issued at the top of a step and consumed in its middle (after the
   // projector): vmcnt retires in issue order, so consuming them at the top of the next step would first
   // wait for all of this step's panel stores.
+  const int home = (int)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (K1_SHARDS - 1));  // XCC_ID
+  auto shard_begin = [&](int x) -> int64_t { return x >= K1_SHARDS ? N : (N * x / K1_SHARDS) / SPW * SPW; };
+  int sh = 0;  // shards (counted from home) found exhausted by this wave
   auto claim_issue = [&]() -> unsigned long long {
     unsigned long long v = 0;
     if (lane == 0) {
-      // an opaque (per-lane) zero offset keeps the atomic optimizer from rewriting the claim as a wave
-      // scan, which reads the returned value (and waits for it) right at the atomic
-      int z;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      // an opaque (per-lane) offset keeps the atomic optimizer from rewriting the claim as a wave scan,
+      // which reads the returned value (and waits for it) right at the atomic
+      int z = 16 * ((home + sh) & (K1_SHARDS - 1));
+      asm volatile("" : "+v"(z));
       v = atomicAdd(work + z, (unsigned long long)SPW);
     }
     return v;
   };
-  auto claim_value = [&](unsigned long long v) -> int64_t {
+  auto uniform64 = [&](unsigned long long v) -> unsigned long long {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (int64_t)(((unsigned long long)hi << 32) | lo);
+    return ((unsigned long long)hi << 32) | lo;
+  };
+  // the sample of a claim issued on the current shard, or (that shard exhausted) the next claim that succeeds
+  // on the following shards, or N when every shard is exhausted
+  auto claim_value = [&](unsigned long long raw) -> int64_t {
+    unsigned long long v = uniform64(raw);
+    bool have = true;  // v is a claim on shard (home + sh)
+    while (sh < K1_SHARDS) {
+      const int x = (home + sh) & (K1_SHARDS - 1);
+      const int64_t b = shard_begin(x), e = shard_begin(x + 1);
+      if (have && b + (int64_t)v < e) return b + (int64_t)v;
+      ++sh;
+      if (sh >= K1_SHARDS) break;
+      const int y = (home + sh) & (K1_SHARDS - 1);
+      unsigned long long seen = 0;
+      if (lane == 0) seen = __hip_atomic_load(work + 16 * y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      have = (int64_t)uniform64(seen) < shard_begin(y + 1) - shard_begin(y);  // else exhausted: no claim
+      if (have) v = uniform64(claim_issue());
+    }
+    return N;
   };
   constexpr int NXR = (192 + HW - 1) / HW;  // input registers per lane (<= 192 channels)
   double xr[NXR];
@@ -659,6 +690,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll
       for (int k = 0; k < 6; ++k) { bj[12 + k] = vi[k]; bj[18 + k] = ai[k]; }
     };
+    if constexpr (!(SYSID_EXP_SKIP & 1)) {  // diagnostics builds may skip this phase (forward kinematics)
     for (int j = 1 + hl; j < NJ; j += HW) {
       const int iq = idx_q[j];
       double RJ[9], tJ[3];
@@ -684,8 +716,10 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         if (depth[j] == lvl) level_step(j);
       wsync();
     }
+    }
     K1_STAMP(1)
 
+    if constexpr (!(SYSID_EXP_SKIP & 2)) {  // diagnostics builds may skip this phase (axes)
     // ---- world motion axes of every dof; contact points ----
     for (int e = hl; e < nv + nc; e += HW) {
       if (e < nv) {
@@ -720,6 +754,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         pfs[3 * c] = x[0] + bj[9]; pfs[3 * c + 1] = x[1] + bj[10]; pfs[3 * c + 2] = x[2] + bj[11];
       }
     }
+    }
     // contacts with a non-zero value as a bit mask (independent loads, no search loop per entry below)
     unsigned long long amask = 0ull;
     for (int c = 0; c < nc; ++c) amask |= (cnt[c] != 0.0 ? 1ull : 0ull) << c;
@@ -728,6 +763,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     K1_STAMP(2)
 
+    if constexpr (!(SYSID_EXP_SKIP & 4)) {  // diagnostics builds may skip this phase (J_c)
     // ---- contact Jacobian (LOCAL_WORLD_ALIGNED, linear rows) ----
     for (int e = hl; e < k * nv; e += HW) {
       const int rho = e / nv, r = e - rho * nv;
@@ -753,6 +789,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     wsync();
 
+    }
     // H1 computed with P by the register-blocked quadruped path (free-flyer dofs 0..5)
     const bool h1_fused = NVC == 18 && HW == 32 && kp.has_ff && kp.ff0 == 0;
     if (kp.full) {
@@ -839,6 +876,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           wsync();
         }
       };
+      if constexpr (!(SYSID_EXP_SKIP & 8)) {  // diagnostics builds may skip this phase (MGS)
       if constexpr (NVC == 18 && HW == 32) {
         if (2 * k <= HW) {
           // Quadruped form: lane pair (2j, 2j+1) keeps its half-row of row j in registers through every
@@ -908,8 +946,10 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       } else {
         mgs_lds();
       }
+      }
       K1_STAMP(4)
 
+      if constexpr (!(SYSID_EXP_SKIP & 16)) {  // diagnostics builds may skip this phase (P)
       // ---- P = I - Q^T Q  (Zt row a = column a of Q; J_c rows = rows of Q) ----
       if constexpr (NVC == 18 && HW == 32) {
         // Register-blocked: lane = (row pair, 6-column group), 27 lanes x 12 entries, every load before
@@ -988,9 +1028,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
         wsync();
       }
+      }
     }
     K1_STAMP(5)
 
+    if constexpr (!(SYSID_EXP_SKIP & 32)) {  // diagnostics builds may skip this phase (tp/H1)
     // ---- tp = P S^T tau  (+ J_c^T lambda in the full mode) ;  H1 = P[:, ff] J_w[:, ff]^T ----
     // tp first: in the full mode H1 may be stored over J_c (overlay layout), which the tau column reads.
     for (int r = hl; r < nv; r += HW) {
@@ -1031,6 +1073,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       H1[e] = h;
     }
     wsync();
+    }
     if (dbg != nullptr && s + half == 0) {
 #ifndef SYSID_STAMPS
       for (int x = hl; x < L.total; x += HW) dbg[x] = wr[x];  // diagnostics: LDS image of sample 0
@@ -1108,6 +1151,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #ifndef SYSID_K1_COLV
 #define SYSID_K1_COLV 2
 #endif
+    if constexpr (!(SYSID_EXP_SKIP & 64)) {  // diagnostics builds may skip this phase (Y_proj columns)
     if constexpr (SYSID_STAGE_Y && NVC == 18 && HW == 32) {
       constexpr int RH = NVC / 2;  // rows per row group
       const bool act = hl < nyi && valid;
@@ -1207,7 +1251,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
     }
 
+    }
     K1_STAMP(8)
+    if constexpr (!(SYSID_EXP_SKIP & 128)) {  // diagnostics builds may skip this phase (friction/torque columns)
     // ---- [B_v | B_c | tau_proj | pad]: lane = (row, column pair), 16-byte stores ----
     {
       const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
@@ -1232,6 +1278,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         if (v2[0] == 1.2345e300) panel_store(out, v2[0], v2[1]);  // diagnostics build
 #endif
       }
+    }
     }
 #if SYSID_PRIO
     __builtin_amdgcn_s_setprio(2);

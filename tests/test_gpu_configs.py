@@ -210,7 +210,7 @@ def test_rejected_launch_enqueues_nothing_and_counter_is_reset():
     bufs["panel"].fill_(-7.0)
     torch.cuda.synchronize()
     import ctypes
-    short = int(e.workspace_bytes(N, EMIT_ALL)) - 256
+    short = int(e.workspace_bytes(N, EMIT_ALL)) - 1024
     rc = e.lib.sysid_build_device(e._h, ctypes.c_void_p(din.data_ptr()), N, din.stride(0), EMIT_ALL,
                                   ctypes.c_void_p(bufs["panel"].data_ptr()), bufs["panel"].stride(0),
                                   ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
@@ -218,7 +218,7 @@ def test_rejected_launch_enqueues_nothing_and_counter_is_reset():
     assert rc == E.SYSID_E_INVALID
     torch.cuda.synchronize()
     assert bool((bufs["panel"] == -7.0).all())  # nothing ran
-    bufs["ws"][:256].fill_(0xA5)  # a counter left mid-count by an aborted launch
+    bufs["ws"][:1024].fill_(0xA5)  # counters left mid-count by an aborted launch
     e.build_device(din, N, EMIT_ALL, bufs)
     torch.cuda.synchronize()
     assert torch.equal(bufs["panel"], P0) and torch.equal(bufs["gram"], G0)
