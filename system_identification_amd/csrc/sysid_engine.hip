@@ -90,9 +90,12 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 
 // K2 split-K: one workgroup per CU and super-tile group; wide Grams (>= 16 tile columns, small row
 // chunks) run two workgroups per CU (measured: G1 K2 -11%, Spot unchanged net of the larger K3).
+#ifndef SYSID_K2_DMA_NARROW
+#define SYSID_K2_DMA_NARROW 0  // experiment: narrow Grams (<= 10 tile columns) on the DMA kernel, 16-row chunks, 2 WG/CU
+#endif
 int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
   // the bf16 kernel's large chunks take most of a CU's LDS: one workgroup per CU
-  const int mult = e->ntc >= 16 && prec != 2 ? 2 : 1;
+  const int mult = (e->ntc >= 16 || (SYSID_K2_DMA_NARROW && e->ntc <= 10)) && prec != 2 ? 2 : 1;
   int ks = std::max(1, mult * e->cus / std::max(1, e->ngroups));
   const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
@@ -204,6 +207,9 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
   return SYSID_OK;
 }
 
+#ifndef SYSID_K2_DMA
+#define SYSID_K2_DMA 1  // 1: LDS-DMA staged, three buffers (k2_gram_syrk_dma); 0: register-staged k2_gram_syrk
+#endif
 int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
               double* slab, hipStream_t st, int prec) {
   if (ld_panel > 16 * e->ntc)
@@ -213,17 +219,32 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
   const float* p32 = static_cast<const float*>(d_panel);
   const __bf16* p16 = static_cast<const __bf16*>(d_panel);
   switch (e->ntc) {
+// f64 / f32 Gram kernels: LDS-DMA staged (three buffers) for wide Grams, register-staged for narrow ones
+// (measured, 20k samples: G1 K2 1.81 -> 1.66 ms with the DMA kernel; Spot 0.202 -> 0.213 ms, so not there).
+#define SYSID_K2_F64(NTC, KC)                                                                                \
+  if constexpr (SYSID_K2_DMA && (NTC >= 16 || (SYSID_K2_DMA_NARROW && NTC <= 10)))                           \
+    hipLaunchKernelGGL((k2_gram_syrk_dma<double, NTC, k2_dma_kc(NTC)>), g2, b2, 0, st, p64, rows, ld_panel,    \
+                       e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                            \
+  else                                                                                                      \
+    hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, e->d_tiles,       \
+                       e->ngroups, ks, e->nslots, accumulate, slab);
+#define SYSID_K2_F32(NTC, KC) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                   \
+  if constexpr (SYSID_K2_DMA && (NTC >= 16 || (SYSID_K2_DMA_NARROW && NTC <= 10)))                           \
+    hipLaunchKernelGGL((k2_gram_syrk_dma<float, NTC, 2 * k2_dma_kc(NTC)>), g2, b2, 0, st, p32, rows, ld_panel, \
+                       e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                            \
+  else                                                                                                      \
+    hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, e->d_tiles,    \
+                       e->ngroups, ks, e->nslots, accumulate, slab);
 #define SYSID_K2_CASE(NTC, KC)                                                                               \
   case NTC:                                                                                                 \
-    if (prec == 0)                                                                                          \
-      hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, e->d_tiles,     \
-                         e->ngroups, ks, e->nslots, accumulate, slab);                                      \
-    else if (prec == 1) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                    \
-      hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, e->d_tiles,  \
-                         e->ngroups, ks, e->nslots, accumulate, slab);                                      \
-    else                                                                                                    \
+    if (prec == 0) {                                                                                        \
+      SYSID_K2_F64(NTC, KC)                                                                                 \
+    } else if (prec == 1) {                                                                                 \
+      SYSID_K2_F32(NTC, KC)                                                                                 \
+    } else {                                                                                                \
       hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, b2, 0, st, p16, rows, ld_panel,       \
                          e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                          \
+    }                                                                                                       \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
     SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)

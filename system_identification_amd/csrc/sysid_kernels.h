@@ -1477,6 +1477,199 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 }
 
 // ------------------------------------------------------------------------------------------------
+// K2, LDS-DMA form (the default for the f64 / f32 Gram): the same super-tiles, k-loop and slab epilogue as
+// k2_gram_syrk above, but the panel chunks go HBM -> LDS by global_load_lds_dwordx4 (no staging registers, no
+// ds_write pass) into THREE LDS buffers, so chunk c + 2 streams in while chunk c is multiplied and chunk c + 1
+// waits complete.  Row rr of a chunk is copied by wave rr % 8 as NP pieces of <= 1 KiB (64 lanes x 16 B; the
+// destination of one instruction is lane-linear, and a row's pieces never cross into the padded stride).  The
+// pipeline spans the per-chunk barrier: a counted `s_waitcnt vmcnt(G)` (G = this wave's DMA instructions per
+// chunk) retires chunk c + 1 and leaves chunk c + 2 in flight, then `lgkmcnt(0)` (this chunk's fragment
+// reads, so its buffer may be refilled) and a raw s_barrier -- never __syncthreads(), whose fence would drain
+// every DMA in flight (cdna_hip_programming.md, "Pipelining across barriers").  All LDS is one __shared__
+// array (a second object made hipcc wait vmcnt(0) before fragment reads, same guide).  The partial last chunk
+// of a row range runs after the pipelined loop: its rows past the range are zero-filled by ds_write.
+// Measured against the register-staged kernel: profiles/r02_*.
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void k2_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// vmcnt(G) for G = RPW * np DMA instructions per chunk (np: pieces per row, 1..3)
+template <int RPW>
+__device__ __forceinline__ void k2_wait_chunk(int np) {
+  if (np == 1) k2_wait_vm<RPW>();
+  else if (np == 2) k2_wait_vm<2 * RPW>();
+  else k2_wait_vm<3 * RPW>();
+}
+__device__ __forceinline__ void k2_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Rows per chunk of the DMA kernel: three buffers of KC x k2_stride(NTC) elements in the CU's 160 KB (one
+// workgroup per CU, NTC < 16) or in half of it (two, NTC >= 16); a multiple of 8 (rows are dealt to the 8 waves).
+#ifndef SYSID_K2_DMA_NARROW
+#define SYSID_K2_DMA_NARROW 0
+#endif
+__host__ __device__ constexpr int k2_dma_kc(int ntc) {
+  return ntc <= 10 ? (SYSID_K2_DMA_NARROW ? 16 : 32) : ntc < 16 ? 24 : 8;
+}
+
+template <typename T, int NTC, int KC>
+__global__ void __launch_bounds__(64 * K2_WAVES)
+k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+                 int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+  typedef typename K2Acc<T>::type accT;
+  static_assert(KC % K2_WAVES == 0 && KC % 4 == 0, "chunk rows are dealt to the 8 waves, k-steps of 4");
+  constexpr int STRIDE = k2_stride(NTC);
+  constexpr int BUF = KC * STRIDE;  // elements per LDS buffer
+  constexpr int NT = 64 * K2_WAVES;
+  constexpr int RPW = KC / K2_WAVES;  // rows per wave per chunk
+  constexpr int EB = (int)sizeof(T);
+  static_assert(3 * BUF * EB <= 160 * 1024, "three LDS buffers");
+  __shared__ __attribute__((aligned(16))) T lds[3 * BUF];
+  const int group = blockIdx.x % ngroups;
+  const int ks = blockIdx.x / ngroups;
+  const int64_t q4 = rows / 4;
+  const int64_t r0 = 4 * (q4 * ks / ksplit);
+  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sbase = (group * K2_WAVES + wave) * K2_SPW;
+
+  // zero the three buffers once: columns >= ldp (up to NTC*16) are never written by the DMA and must read as 0
+  for (int x = threadIdx.x; x < 3 * BUF; x += NT) lds[x] = (T)0;
+
+  const int rowbytes = (int)ldp * EB;             // <= STRIDE * EB
+  const int np = (rowbytes + 1023) >> 10;         // 1 KiB pieces per row (wave-uniform, 1..3)
+  constexpr int NPMAX = (16 * NTC * EB + 1023) / 1024;
+  auto dma_row = [&](const T* src_row, T* dst_row) {
+    const char* src = reinterpret_cast<const char*>(src_row);
+    char* dst = reinterpret_cast<char*>(dst_row);
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) {
+      if (p < np) {  // wave-uniform; every piece below np has >= 1 live lane: exactly np instructions per row
+        const int off = (p << 10) + 16 * lane;
+        if (off < rowbytes)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
+                                           reinterpret_cast<void*>(dst + (p << 10)), 16, 0, 0);
+      }
+    }
+  };
+  auto dma_chunk = [&](int64_t c0, T* buf) {  // RPW * np instructions per wave
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave + K2_WAVES * q;
+      dma_row(panel + (c0 + rr) * ldp, buf + rr * STRIDE);
+    }
+  };
+
+  int foff[4 * K2_SPW];
+  bool live[K2_SPW];
+  bool need[K2_SPW][4];
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s) {
+    int2 sp = supers[sbase + s];
+    live[s] = sp.x >= 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int I = 2 * sp.x + (t >> 1), J = 2 * sp.y + (t & 1);
+      need[s][t] = live[s] && I <= J && J < NTC;
+    }
+    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
+      foff[4 * s + u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
+    }
+  }
+  accT acc[K2_SPW][4];
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
+  auto mfma_chunk = [&](const T* cur) {
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      T x[4 * K2_SPW];
+#pragma unroll
+      for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = cur[foff[u] + kk * STRIDE];
+#pragma unroll
+      for (int s = 0; s < K2_SPW; ++s) {
+        constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (!need[s][t]) continue;
+          if constexpr (sizeof(T) == 8)
+            acc[s][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
+          else
+            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  const int64_t nfull = (r1 - r0) / KC;  // whole chunks; then one partial chunk if rows remain
+  __syncthreads();                        // LDS zeroed (no DMA in flight yet)
+  T* b0 = lds;                            // chunk c
+  T* b1 = lds + BUF;                      // chunk c + 1
+  T* b2 = lds + 2 * BUF;                  // chunk c + 2
+  if (nfull > 0) dma_chunk(r0, b0);
+  if (nfull > 1) {
+    dma_chunk(r0 + KC, b1);
+    k2_wait_chunk<RPW>(np);  // chunk 0 landed (chunk 1 in flight)
+  } else {
+    k2_wait_vm<0>();
+  }
+  k2_barrier();
+  for (int64_t c = 0; c < nfull; ++c) {
+    const bool pre = c + 2 < nfull;
+    if (pre) dma_chunk(r0 + (c + 2) * KC, b2);
+    mfma_chunk(b0);
+    if (pre) k2_wait_chunk<RPW>(np);  // chunk c + 1 landed, chunk c + 2 stays in flight
+    else k2_wait_vm<0>();
+    k2_barrier();                     // ... for every wave; b0's fragment reads retired (it is refilled next)
+    T* t = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = t;
+  }
+  if (r0 + nfull * KC < r1) {  // the partial last chunk, into b0 (free: its last chunk finished two barriers ago)
+    const int64_t c0 = r0 + nfull * KC;
+    const int valid = (int)(r1 - c0);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave + K2_WAVES * q;
+      T* dst = b0 + rr * STRIDE;
+      if (rr < valid) {
+        dma_row(panel + (c0 + rr) * ldp, dst);
+      } else {
+        for (int x = 16 * lane; x < rowbytes; x += 16 * 64) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst) + x) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    k2_wait_vm<0>();
+    k2_barrier();
+    mfma_chunk(b0);
+  }
+  // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
+#pragma unroll
+  for (int s = 0; s < K2_SPW; ++s) {
+    if (!live[s]) continue;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = sizeof(T) == 8 ? (lane >> 4) + 4 * j : 4 * (lane >> 4) + j;
+        double* x = o + row * 16 + (lane & 15);
+        const double v = (double)acc[s][t][j];
+        *x = accumulate ? *x + v : v;  // chunked Gram: slabs carry over chunks
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // K2 bf16: the same super-tile decomposition on v_mfma_f32_16x16x32_bf16, from a bf16 panel (K1 rounds the
 // Gram-only chunk panel to bf16 as it writes it; ld a multiple of 8).  A chunk of KC (a multiple of 32) rows is
 // staged column-major in LDS (column stride CS = KC + 8 bf16), so the fragment of lane l — 8 consecutive rows
