@@ -1254,9 +1254,43 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     K1_STAMP(8)
     if constexpr (!(SYSID_EXP_SKIP & 128)) {  // diagnostics builds may skip this phase (friction/torque columns)
-    // ---- [B_v | B_c | tau_proj | pad]: lane = (row, column pair), 16-byte stores ----
-    {
-      const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
+    // ---- [B_v | B_c | tau_proj | pad]: 16-byte stores of column pairs ----
+    // Up to 32 pairs (nj <= 31): lane = column pair m within a 32-lane group, the groups taking every
+    // (HW/32)-th row, so a lane's dq / sign(dq) factors and column selects are fixed over its rows; otherwise
+    // lane = (row, column pair) with a division per item.
+    const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
+    if (npair <= 32) {
+      constexpr int NG = HW / 32;
+      const int fg = hl >> 5, m = hl & 31;
+      if (m < npair && valid) {
+        int jc[2];
+        double sc[2];
+        bool tcol[2], fcol[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int jj = 2 * m + u;  // column - wy
+          const bool coul = jj >= nja;
+          const int j = coul ? jj - nja : jj;
+          jc[u] = j < nja ? j : nja - 1;  // clamp for the tau/pad columns
+          const double x = dqs[bd + jc[u]];
+          sc[u] = coul ? sign_of(x) : x;
+          fcol[u] = jj < 2 * nja;
+          tcol[u] = kp.wy + jj == kp.w;
+        }
+        for (int r = fg; r < nv; r += NG) {
+          const double* pr = Ps + r * nv + bd;
+          const double t = tps[r];
+          double v2[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pr[jc[u]] * sc[u] : (tcol[u] ? t : 0.0);  // pad: whole lines
+#ifndef SYSID_EXP_NO_FSTORE
+          panel_store(out + (int64_t)r * ldp + kp.wy + 2 * m, v2[0], v2[1]);
+#else
+          if (v2[0] == 1.2345e300) panel_store(out, v2[0], v2[1]);  // diagnostics build
+#endif
+        }
+      }
+    } else {
       for (int it = hl; it < nv * npair && valid; it += HW) {
         const int r = it / npair, m = it - r * npair;
         const double* pr = Ps + r * nv + bd;
