@@ -1277,14 +1277,16 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           fcol[u] = jj < 2 * nja;
           tcol[u] = kp.wy + jj == kp.w;
         }
-        for (int r = fg; r < nv; r += NG) {
+        OutT* po = out + (int64_t)fg * ldp + kp.wy + 2 * m;  // advanced by NG rows per pass
+        const int64_t pstep = (int64_t)NG * ldp;
+        for (int r = fg; r < nv; r += NG, po += pstep) {
           const double* pr = Ps + r * nv + bd;
           const double t = tps[r];
           double v2[2];
 #pragma unroll
           for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pr[jc[u]] * sc[u] : (tcol[u] ? t : 0.0);  // pad: whole lines
 #ifndef SYSID_EXP_NO_FSTORE
-          panel_store(out + (int64_t)r * ldp + kp.wy + 2 * m, v2[0], v2[1]);
+          panel_store(po, v2[0], v2[1]);
 #else
           if (v2[0] == 1.2345e300) panel_store(out, v2[0], v2[1]);  // diagnostics build
 #endif
