@@ -1222,10 +1222,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         wsync();
         if (valid) {
           const double2* s2 = reinterpret_cast<const double2*>(stg);
+          // pair x of row group gg lands at row gg*RH + rho, column 2*(x - gg*wy2): from this row's start
+          // that is 2x, plus dg for the second group (one select and add per store, no 64-bit multiply)
+          OutT* orow = out + (int64_t)rho * ldp;
+          const int dg = RH * (int)ldp - kp.wy;
           for (int x = hl; x < n2; x += HW) {
-            const int gg = x >= wy2 ? 1 : 0, c2 = x - gg * wy2;
 #ifndef SYSID_EXP_NO_YSTORE
-            panel_store(out + (int64_t)(gg * RH + rho) * ldp + 2 * c2, s2[x].x, s2[x].y);
+            panel_store(orow + 2 * x + (x >= wy2 ? dg : 0), s2[x].x, s2[x].y);
 #else
             if (s2[x].x == 1.2345e300) panel_store(out, s2[x].x, s2[x].y);  // diagnostics build: keep the reads
 #endif
