@@ -1185,6 +1185,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       wsync();  // every read of the joint records precedes the first staging store
       double* stg = body;  // [row group][wy]
       const int wy2 = kp.wy >> 1, n2 = kp.rg * wy2;
+#ifndef SYSID_K1_YST_SBASE
+#define SYSID_K1_YST_SBASE 1
+#endif
+#if SYSID_K1_YST_SBASE
+      char* ybase = reinterpret_cast<char*>(panel + (s * NVC) * ldp);
+      const uint32_t yhoff = (uint32_t)(half * NVC * (int)ldp * (int)sizeof(OutT));
+#endif
 #pragma unroll 1
       for (int rho = 0; rho < RH; ++rho) {
         if (act) {
@@ -1223,12 +1230,23 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         if (valid) {
           const double2* s2 = reinterpret_cast<const double2*>(stg);
           // pair x of row group gg lands at row gg*RH + rho, column 2*(x - gg*wy2): from this row's start
-          // that is 2x, plus dg for the second group (one select and add per store, no 64-bit multiply)
-          OutT* orow = out + (int64_t)rho * ldp;
+          // that is 2x, plus dg for the second group.  The row start of the wave's first sample is
+          // wave-uniform (scalar registers); the second sample's rows and the column go into a 32-bit lane
+          // byte offset, so each store is a scalar-base + lane-offset store with no 64-bit address math.
           const int dg = RH * (int)ldp - kp.wy;
+#if SYSID_K1_YST_SBASE
+          char* rb = ybase + (int64_t)rho * ldp * (int64_t)sizeof(OutT);
+#else
+          OutT* orow = out + (int64_t)rho * ldp;
+#endif
           for (int x = hl; x < n2; x += HW) {
 #ifndef SYSID_EXP_NO_YSTORE
+#if SYSID_K1_YST_SBASE
+            const uint32_t off = yhoff + (uint32_t)((2 * x + (x >= wy2 ? dg : 0)) * (int)sizeof(OutT));
+            panel_store(reinterpret_cast<OutT*>(rb + off), s2[x].x, s2[x].y);
+#else
             panel_store(orow + 2 * x + (x >= wy2 ? dg : 0), s2[x].x, s2[x].y);
+#endif
 #else
             if (s2[x].x == 1.2345e300) panel_store(out, s2[x].x, s2[x].y);  // diagnostics build: keep the reads
 #endif
