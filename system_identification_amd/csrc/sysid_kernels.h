@@ -631,55 +631,30 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     K1_STAMP(0)
 
-    // ---- forward pass (computeJointTorqueRegressor forward step) + placements ----
-    // Joint placements liMi = jointPlacement * M_J(q) of every joint at once (one lane per joint: the
-    // sincos / quaternion work is off the depth-serial path), parked in the joint's own pose slot.
-    // Forward step of joint j from its parent's record (its liMi is in its own record, from the placement
-    // pass below).
-    auto level_step = [&](int j) {
-      const int p = parent[j];
-      const int iv = idx_v[j];
-      const double* bp = body + BODY_STRIDE * p;
+    // ---- forward pass (computeJointTorqueRegressor forward step), in two parts ----
+    // (1) here: joint placements liMi = jointPlacement * M_J(q) of every joint at once (one lane per joint:
+    //     the sincos / quaternion work is off the depth-serial path), parked in the joint's own pose slot,
+    //     then the poses level by level, oR_j = oR_p liR_j, ot_j = oR_p lit_j + ot_p: the only depth-serial
+    //     work, 36 FMAs per level;
+    // (2) after the motion axes (below): every joint's velocity and acceleration at once, one lane per
+    //     joint, as sums over its chain.
+    // Poses are kept relative to the free-flyer (base) frame, not the world: the regressor rows of
+    // pinocchio only see the base rotation through R_b^T g, and J_c's row space (hence P) is the same in
+    // base-aligned and world-aligned axes because R_b is invertible.  This stays exact for the float32,
+    // slightly non-unit quaternions of the reference's .dat logs.
+    auto pose_step = [&](int j) {
+      const double* bp = body + BODY_STRIDE * parent[j];
       double* bj = body + BODY_STRIDE * j;
-      double liR[9], lit[3], vJ[6], Sa[6];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) liR[k] = bj[k];
-      lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
-      const bool ff = jtype[j] == JT_FREEFLYER;
-      if (ff) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) { vJ[k] = dq[iv + k]; Sa[k] = ddq[iv + k]; }
-      } else {
-        const double* ax = axis + 3 * j;
-        const double w = dq[iv], aa = ddq[iv];
-        vJ[0] = vJ[1] = vJ[2] = 0.0; Sa[0] = Sa[1] = Sa[2] = 0.0;
-        vJ[3] = ax[0] * w; vJ[4] = ax[1] * w; vJ[5] = ax[2] * w;
-        Sa[3] = ax[0] * aa; Sa[4] = ax[1] * aa; Sa[5] = ax[2] * aa;
-      }
-      double vp[6], ap[6], vi[6], ai[6], c1[3], c2[3];
-      act_inv_motion(liR, lit, bp + 12, vp);
-      act_inv_motion(liR, lit, bp + 18, ap);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) vi[k] = vJ[k] + vp[k];
-      if (ff) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) ai[k] = Sa[k] + ap[k];  // v x v = 0
-      } else {
-        cross3(vi, vJ + 3, c1);      // motion cross v x vJ with vJ = (0, wJ)
-        cross3(vi + 3, vJ + 3, c2);
-        ai[0] = c1[0] + Sa[0] + ap[0]; ai[1] = c1[1] + Sa[1] + ap[1]; ai[2] = c1[2] + Sa[2] + ap[2];
-        ai[3] = c2[0] + Sa[3] + ap[3]; ai[4] = c2[1] + Sa[4] + ap[4]; ai[5] = c2[2] + Sa[5] + ap[5];
-      }
-      // Poses are kept relative to the free-flyer (base) frame, not the world: the regressor rows of
-      // pinocchio only see the base rotation through R_b^T g (its actInv above), and J_c's row space
-      // (hence P) is the same in base-aligned and world-aligned axes because R_b is invertible.  This
-      // stays exact for the float32, slightly non-unit quaternions of the reference's .dat logs.
       double oR[9], ot[3];
-      if (ff) {
+      if (jtype[j] == JT_FREEFLYER) {
         oR[0] = 1.0; oR[1] = 0.0; oR[2] = 0.0; oR[3] = 0.0; oR[4] = 1.0; oR[5] = 0.0;
         oR[6] = 0.0; oR[7] = 0.0; oR[8] = 1.0;
         ot[0] = ot[1] = ot[2] = 0.0;
       } else {
+        double liR[9], lit[3];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) liR[k] = bj[k];
+        lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
         mat3mul(bp, liR, oR);
         mat3vec(bp, lit, ot);
         ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
@@ -687,8 +662,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll
       for (int k = 0; k < 9; ++k) bj[k] = oR[k];
       bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) { bj[12 + k] = vi[k]; bj[18 + k] = ai[k]; }
     };
     if constexpr (!(SYSID_EXP_SKIP & 1)) {  // diagnostics builds may skip this phase (forward kinematics)
     for (int j = 1 + hl; j < NJ; j += HW) {
@@ -706,14 +679,14 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       mat3mul(R0 + 9 * j, RJ, bj);
       mat3vec(R0 + 9 * j, tJ, tmp);
       bj[9] = tmp[0] + t0[3 * j]; bj[10] = tmp[1] + t0[3 * j + 1]; bj[11] = tmp[2] + t0[3 * j + 2];
-      if (depth[j] == 1) level_step(j);
+      if (depth[j] == 1) pose_step(j);
     }
     wsync();
-    // Velocities / accelerations level by level (a joint's parent is one level up); level 1 (parent = the
-    // universe, whose record is set at the top of the step) runs in the placement pass.
+    // Poses level by level (a joint's parent is one level up); level 1 (parent = the universe, whose
+    // record is set at the top of the step) runs in the placement pass.
     for (int lvl = 2; lvl <= kp.maxdepth; ++lvl) {
       for (int j = 1 + hl; j < NJ; j += HW)
-        if (depth[j] == lvl) level_step(j);
+        if (depth[j] == lvl) pose_step(j);
       wsync();
     }
     }
@@ -753,6 +726,65 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         mat3vec(bj, ct + 3 * c, x);
         pfs[3 * c] = x[0] + bj[9]; pfs[3 * c + 1] = x[1] + bj[10]; pfs[3 * c + 2] = x[2] + bj[11];
       }
+    }
+    }
+    if constexpr (!(SYSID_EXP_SKIP & 1)) {  // diagnostics builds may skip this phase (forward kinematics)
+    // ---- forward pass, part (2): body velocities and accelerations ----
+    // In base coordinates (the free-flyer frame) the recursion a_j = X_jp a_p + S_j ddq_j + v_j x S_j dq_j
+    // reads A_j = A_p + S_d ddq_d + V_p x S_d dq_d (the adjoint commutes with the motion cross product, and
+    // v_j x S_j dq_j = v_p x S_j dq_j), with S_d = Jws row d.  So per joint, over its revolute chain d (root
+    // side first):  A += S_d ddq_d + V x S_d dq_d,  V += S_d dq_d,  from V_0 / A_0 = the free-flyer's
+    // dq / ddq + R_b^T (-g) (its own frame: pinocchio's local free-flyer velocity), or (0, -g) for a joint
+    // under the fixed base; then v_j = V.actInv(oM_j), a_gf_j = A.actInv(oM_j).  One lane per joint, no
+    // depth-serial passes.  (A joint hangs under the free-flyer iff its depth exceeds its revolute chain.)
+    wsync();  // Jws rows of other lanes
+    for (int j = 1 + hl; j < NJ; j += HW) {
+      double V[6], A[6];
+      const int cl = chain_len[j];
+      if (kp.has_ff && depth[j] > cl) {
+        const int jf = dof_joint[kp.ff0], iq = idx_q[jf], iv = kp.ff0;
+        double Rb[9], mg[3] = {-kp.g0, -kp.g1, -kp.g2}, gb[3];
+        quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], Rb);
+        mat3tvec(Rb, mg, gb);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          V[k] = dq[iv + k];
+          V[3 + k] = dq[iv + 3 + k];
+          A[k] = ddq[iv + k] + gb[k];
+          A[3 + k] = ddq[iv + 3 + k];
+        }
+      } else {
+        A[0] = -kp.g0; A[1] = -kp.g1; A[2] = -kp.g2;
+        V[0] = V[1] = V[2] = V[3] = V[4] = V[5] = A[3] = A[4] = A[5] = 0.0;
+      }
+      const int* ch = chain + j * kp.maxch;
+      for (int t = 0; t < cl; ++t) {
+        const int d = ch[t];
+        const double* S = Jws + 6 * d;
+        const double qd = dq[d], qdd = ddq[d];
+        double Sd[6], sv[6], c1[3], c2[3], c3[3];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          Sd[k] = S[k];
+          sv[k] = Sd[k] * qd;
+        }
+        cross3(V + 3, sv, c1);      // w x s_lin
+        cross3(V, sv + 3, c2);      // v x s_ang
+        cross3(V + 3, sv + 3, c3);  // w x s_ang
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          A[k] += Sd[k] * qdd + (c1[k] + c2[k]);
+          A[3 + k] += Sd[3 + k] * qdd + c3[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) V[k] += sv[k];
+      }
+      double* bj = body + BODY_STRIDE * j;
+      double vb[6], ab[6];
+      act_inv_motion(bj, bj + 9, V, vb);
+      act_inv_motion(bj, bj + 9, A, ab);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { bj[12 + k] = vb[k]; bj[18 + k] = ab[k]; }
     }
     }
     // contacts with a non-zero value as a bit mask (independent loads, no search loop per entry below)
