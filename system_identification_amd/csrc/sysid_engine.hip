@@ -101,14 +101,8 @@ int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
   return (int)std::min<int64_t>(ks, cap);
 }
 
-int rsplit_for(int ks) { return std::min(ks, 16); }
-
 size_t slab_bytes(const sysid_engine* e, int64_t rows) {
   return align256((size_t)ksplit_for(e, rows) * e->nslots * 256 * sizeof(double));
-}
-
-size_t part_bytes(const sysid_engine* e, int64_t rows) {
-  return align256((size_t)rsplit_for(ksplit_for(e, rows)) * e->nslots * 256 * sizeof(double));
 }
 
 int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
@@ -207,6 +201,9 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
   return SYSID_OK;
 }
 
+#ifndef SYSID_K2_KC10
+#define SYSID_K2_KC10 32  // rows per chunk of the register-staged kernel at 10 tile columns (Spot)
+#endif
 #ifndef SYSID_K2_DMA
 #define SYSID_K2_DMA 1  // 1: LDS-DMA staged, three buffers (k2_gram_syrk_dma); 0: register-staged k2_gram_syrk
 #endif
@@ -247,7 +244,7 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
     }                                                                                                       \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
-    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
+    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, SYSID_K2_KC10)
     SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20)
     SYSID_K2_CASE(15, 20) SYSID_K2_CASE(16, 12) SYSID_K2_CASE(17, 12) SYSID_K2_CASE(18, 12)
     SYSID_K2_CASE(19, 12) SYSID_K2_CASE(20, 12) SYSID_K2_CASE(21, 8) SYSID_K2_CASE(22, 8)
@@ -260,23 +257,19 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
   return SYSID_OK;
 }
 
-int launch_k3(sysid_engine* e, int ks, const double* slab, double* part, double* d_gram, hipStream_t st) {
-  const int rs = rsplit_for(ks);
+int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st) {
   const int64_t nx = (int64_t)e->nslots * 256;
-  hipLaunchKernelGGL(k3_gram_partial, dim3((unsigned)((nx + 255) / 256), rs), dim3(256), 0, st, slab, nx, ks, rs,
-                     part);
-  HIP_TRY(e, hipGetLastError());
-  hipLaunchKernelGGL(k3_gram_final, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, st, part,
-                     e->d_tiles + e->nsuper, e->nslots, rs, e->ncol, d_gram);
+  hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, e->d_tiles + e->nsuper, nx,
+                     ks, e->ncol, d_gram);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
 
-// Workspace of sysid_build_device: [K1 counter | K2 slabs | K3 partials] (the last two with EMIT_GRAM).
+// Workspace of sysid_build_device: [K1 counter | K2 slabs] (the slabs with EMIT_GRAM).
 size_t stages_ws_bytes(const sysid_engine* e, int64_t N, uint32_t flags) {
   if (N <= 0) return 0;
   const int64_t rows = N * e->nv;
-  return WORK_BYTES + ((flags & SYSID_EMIT_GRAM) ? slab_bytes(e, rows) + part_bytes(e, rows) : 0);
+  return WORK_BYTES + ((flags & SYSID_EMIT_GRAM) ? slab_bytes(e, rows) : 0);
 }
 
 // Every check of a launch sequence happens before its first enqueue: an error return means nothing was
@@ -309,10 +302,9 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   if (flags & SYSID_EMIT_GRAM) {
     const int ks = ksplit_for(e, rows);
     double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-    double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows));
     if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
-    if ((rc = launch_k3(e, ks, slab, part, d_gram, st)) != SYSID_OK) return rc;
+    if ((rc = launch_k3(e, ks, slab, d_gram, st)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
   } else if (ev) {
     HIP_TRY(e, hipEventRecord(ev[2], st));
@@ -345,11 +337,10 @@ int64_t gram_chunk(const sysid_engine* e, int64_t N, int prec) {
   return std::max<int64_t>(1, std::min(c, N));
 }
 
-// [K1 counter | panel chunk | K2 slabs | K3 partials]
+// [K1 counter | panel chunk | K2 slabs]
 size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
   const int64_t rows = gram_chunk(e, N, prec) * e->nv;
-  return WORK_BYTES + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) + slab_bytes(e, rows) +
-         part_bytes(e, rows);
+  return WORK_BYTES + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) + slab_bytes(e, rows);
 }
 
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
@@ -369,7 +360,6 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   auto* work = static_cast<unsigned long long*>(d_ws);
   char* panel = static_cast<char*>(d_ws) + WORK_BYTES;
   double* slab = reinterpret_cast<double*>(panel + align256((size_t)rows0 * ldc * prec_bytes(prec)));
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows0));
   const int ks0 = ksplit_for(e, rows0, prec);  // <= ksplit_for(e, rows0): the slabs fit the workspace
   int rc;
   size_t k = 0;
@@ -385,7 +375,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     if ((rc = launch_k2(e, panel, n * e->nv, ldc, ks, c0 > 0, slab, st, prec)) != SYSID_OK) return rc;
   }
   if ((rc = mark())) return rc;
-  if ((rc = launch_k3(e, ks0, slab, part, d_gram, st))) return rc;
+  if ((rc = launch_k3(e, ks0, slab, d_gram, st))) return rc;
   return mark();
 }
 
@@ -1124,9 +1114,8 @@ int32_t sysid_exp_k2(sysid_engine* e, const double* d_panel, int64_t N, int64_t 
   const int64_t rows = N * e->nv;
   const int ks = ksplit_for(e, rows);
   double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows));
   int rc = launch_k2(e, d_panel, rows, ld_panel, ks, accumulate, slab, st, 0);
-  if (rc == SYSID_OK && final) rc = launch_k3(e, ks, slab, part, d_gram, st);
+  if (rc == SYSID_OK && final) rc = launch_k3(e, ks, slab, d_gram, st);
   return rc;
 }
 int32_t sysid_exp_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,

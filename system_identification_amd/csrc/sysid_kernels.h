@@ -8,7 +8,7 @@
 //                       contiguous sample ranges with the next sample's inputs prefetched.
 //   k2_gram_syrk        split-K SYRK of the panel on v_mfma_f64_16x16x4_f64 (upper 16x16 tiles),
 //                       8 waves, register-staged double-buffered row chunks in LDS.
-//   k3_gram_partial / k3_gram_final   deterministic two-level sum of the K2 slabs -> symmetric Gram.
+//   k3_gram_reduce      deterministic one-pass sum of the K2 slabs -> symmetric Gram.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -1916,41 +1916,41 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
   }
 }
 
-// K3a: part[r][x] = sum of slab[ks][x] over ks in split r  (x = slot*256 + element)
-__global__ void __launch_bounds__(256)
-k3_gram_partial(const double* __restrict__ slab, int64_t nx, int ksplit, int rsplit, double* __restrict__ part) {
-  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int r = blockIdx.y;
-  if (x >= nx) return;
-  const int k0 = ksplit * r / rsplit, k1 = ksplit * (r + 1) / rsplit;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int ks = k0;
-  for (; ks + 4 <= k1; ks += 4) {
-    a0 += slab[(size_t)ks * nx + x];
-    a1 += slab[(size_t)(ks + 1) * nx + x];
-    a2 += slab[(size_t)(ks + 2) * nx + x];
-    a3 += slab[(size_t)(ks + 3) * nx + x];
+// K3, one pass: G = the sum of the ksplit slabs, in a fixed order, mirrored.  A workgroup of 16 waves owns 64
+// consecutive entries of one tile slot (so a dead slot drops the whole workgroup); wave w sums slabs w, w + 16,
+// ... with eight loads in flight per lane, and the 16 wave sums are added in LDS as a fixed pairwise tree.
+// Every slab byte is requested by a quarter of a million lanes at once: the pass is one HBM read of the
+// slabs, with no partial-sum round trip and no second launch.
+__global__ void __launch_bounds__(1024)
+k3_gram_reduce(const double* __restrict__ slab, const int2* __restrict__ tiles, int64_t nx, int ksplit, int ncol,
+               double* __restrict__ G) {
+  __shared__ double red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int2 ij = tiles[(int)(e >> 8)];
+  if (ij.x < 0) return;  // workgroup-uniform: the 64 entries share one slot
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int ks = wave;
+  for (; ks + 7 * 16 < ksplit; ks += 8 * 16) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += slab[(size_t)(ks + 16 * u) * nx + e];
   }
-  for (; ks < k1; ++ks) a0 += slab[(size_t)ks * nx + x];
-  part[(size_t)r * nx + x] = (a0 + a1) + (a2 + a3);
-}
-
-// K3b: G[I*16+r][J*16+c] = sum_r part[r][slot][r*16+c], mirrored.
-__global__ void __launch_bounds__(256)
-k3_gram_final(const double* __restrict__ part, const int2* __restrict__ tiles, int nslots, int rsplit, int ncol,
-              double* __restrict__ G) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nx = (int64_t)nslots * 256;
-  if (e >= nx) return;
-  const int t = (int)(e >> 8), x = (int)(e & 255);
-  const int2 ij = tiles[t];
-  if (ij.x < 0) return;
-  double acc = 0.0;
-  for (int r = 0; r < rsplit; ++r) acc += part[(size_t)r * nx + e];
-  const int gi = ij.x * 16 + (x >> 4), gj = ij.y * 16 + (x & 15);
-  if (gi < ncol && gj < ncol) {
-    G[(int64_t)gi * ncol + gj] = acc;
-    G[(int64_t)gj * ncol + gi] = acc;
+  for (; ks < ksplit; ks += 16) a[0] += slab[(size_t)ks * nx + e];
+  red[wave][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+#pragma unroll
+  for (int h = 8; h >= 1; h >>= 1) {
+    if (wave < h) red[wave][lane] += red[wave + h][lane];
+    __syncthreads();
+  }
+  if (wave == 0) {
+    const int x = (int)(e & 255);
+    const int gi = ij.x * 16 + (x >> 4), gj = ij.y * 16 + (x & 15);
+    if (gi < ncol && gj < ncol) {
+      const double acc = red[0][lane];
+      G[(int64_t)gi * ncol + gj] = acc;
+      G[(int64_t)gj * ncol + gi] = acc;
+    }
   }
 }
 
