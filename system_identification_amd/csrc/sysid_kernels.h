@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace sysid_dev {
 
@@ -1389,7 +1390,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 // panel is one contiguous byte range in HBM; every thread copies fixed double2 slots of it (offsets
 // computed once, no divisions in the loop) through registers into an LDS buffer with a padded row
 // stride (STRIDE ≡ 16 mod 32 doubles, so the 2 rows x 16 doubles of a 32-lane ds_read_b64 group hit
-// disjoint banks).  Two LDS buffers: chunk c+1's global loads are in flight while chunk c is multiplied.
+// disjoint banks).  Two LDS buffers and two staging register sets: chunk c+2's global loads are in flight
+// while chunk c is multiplied and chunk c+1 is written to LDS.
 // Each wave owns K2_SPW "super-tiles" (2x2 blocks of 16x16 output tiles): 4 fragment reads feed 4 MFMAs.
 // The k-loop over a chunk is fully unrolled, so fragment reads use immediate LDS offsets.
 // Fragment = 16 consecutive doubles of 4 consecutive rows: lane l holds row (l>>4), col (l&15), which is
@@ -1436,9 +1438,10 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   __shared__ T lds[2 * BUF];
   const int group = blockIdx.x % ngroups;
   const int ks = blockIdx.x / ngroups;
-  const int64_t q4 = rows / 4;
-  const int64_t r0 = 4 * (q4 * ks / ksplit);
-  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
+  // whole chunks per workgroup: only the panel's last chunk may be partial
+  const int64_t nck = (rows + KC - 1) / KC;
+  const int64_t r0 = (nck * ks / ksplit) * KC;
+  const int64_t r1 = ks + 1 == ksplit ? rows : (nck * (ks + 1) / ksplit) * KC;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int sbase = (group * K2_WAVES + wave) * K2_SPW;
 
@@ -1512,16 +1515,13 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
 
-  const int64_t nchunks = (r1 - r0 + KC - 1) / KC;
-  __syncthreads();  // LDS zeroed
-  if (nchunks > 0) {
-    load_chunk(r0);
-    store_chunk(lds);
-  }
-  __syncthreads();
-  for (int64_t c = 0; c < nchunks; ++c) {
-    const T* cur = lds + (c & 1) * BUF;
-    if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * KC);
+  // Loads run two chunks ahead through two register sets: chunk c + 2 is requested while chunk c is
+  // multiplied and chunk c + 1 (requested one chunk earlier) is written to the other LDS buffer, so each
+  // load has about two chunks of MFMA time to land.  Every load is unconditional (past the last full chunk
+  // the index is clamped: a reload of a chunk just read, from L2), so the compiler's vmcnt bookkeeping
+  // waits only for the set being stored.  The partial tail chunk of the panel's last workgroup runs last,
+  // zero-filled.
+  auto mfma_chunk = [&](const T* cur) {
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
       T x[4 * K2_SPW];
@@ -1544,8 +1544,55 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
         }
       }
     }
-    if (c + 1 < nchunks) store_chunk(lds + ((c + 1) & 1) * BUF);
+  };
+  const int64_t nfull = (r1 - r0) / KC;
+  uint4 sa[PER], sb[PER];  // the two staging register sets (selected at compile time)
+  auto load_full = [&](int64_t c, auto set) {
+    constexpr int S = decltype(set)::value;
+    const int64_t cc = c < nfull ? c : nfull - 1;
+    const uint4* src = reinterpret_cast<const uint4*>(panel + (r0 + cc * KC) * ldp);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {  // unconditional (an unused slot re-reads the chunk's last 16 bytes)
+      const int x = (int)threadIdx.x + u * NT;
+      const uint4 v = src[x < chunk_s ? x : chunk_s - 1];
+      if constexpr (S == 0) sa[u] = v; else sb[u] = v;
+    }
+  };
+  auto store_set = [&](auto set, T* b) {
+    constexpr int S = decltype(set)::value;
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+      if (used[u]) *reinterpret_cast<uint4*>(b + loff[u]) = S == 0 ? sa[u] : sb[u];
+  };
+  constexpr std::integral_constant<int, 0> A{};
+  constexpr std::integral_constant<int, 1> B{};
+  __syncthreads();  // LDS zeroed
+  if (nfull > 0) {
+    load_full(0, A);
+    load_full(1, B);
+    store_set(A, lds);
+  }
+  __syncthreads();
+  int64_t c = 0;
+  for (; c + 1 < nfull; c += 2) {  // chunks c (buffer 0, set A) and c + 1 (buffer 1, set B)
+    load_full(c + 2, A);
+    mfma_chunk(lds);
+    store_set(B, lds + BUF);
     __syncthreads();
+    load_full(c + 3, B);
+    mfma_chunk(lds + BUF);
+    if (c + 2 < nfull) store_set(A, lds);
+    __syncthreads();
+  }
+  if (c < nfull) {  // an odd last full chunk, already in buffer 0
+    mfma_chunk(lds);
+    __syncthreads();
+  }
+  if (r0 + nfull * KC < r1) {  // the panel's partial last chunk
+    load_chunk(r0 + nfull * KC);
+    store_chunk(lds);
+    __syncthreads();
+    mfma_chunk(lds);
   }
   // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
 #pragma unroll
