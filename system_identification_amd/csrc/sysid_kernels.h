@@ -1309,13 +1309,15 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     K1_STAMP(8)
     if constexpr (!(SYSID_EXP_SKIP & 128)) {  // diagnostics builds may skip this phase (friction/torque columns)
     // ---- [B_v | B_c | tau_proj | pad]: 16-byte stores of column pairs ----
-    // Up to 32 pairs (nj <= 31): lane = column pair m within a 32-lane group, the groups taking every
-    // (HW/32)-th row, so a lane's dq / sign(dq) factors and column selects are fixed over its rows; otherwise
-    // lane = (row, column pair) with a division per item.
+    // Up to 32 pairs (nj <= 31): lane = column pair m within a group of gs = 8, 16 or 32 lanes (the
+    // narrowest that holds the pairs), the HW/gs groups taking every (HW/gs)-th row, so a lane's dq / sign(dq)
+    // factors and column selects are fixed over its rows (Spot: 15 pairs, two 16-lane groups, 9 rows each);
+    // otherwise lane = (row, column pair) with a division per item.
     const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
     if (npair <= 32) {
-      constexpr int NG = HW / 32;
-      const int fg = hl >> 5, m = hl & 31;
+      const int lg = npair <= 8 ? 3 : (npair <= 16 ? 4 : 5);  // log2 of the group width
+      const int NG = HW >> lg;
+      const int fg = hl >> lg, m = hl & ((1 << lg) - 1);
       if (m < npair && valid) {
         int jc[2];
         double sc[2];
