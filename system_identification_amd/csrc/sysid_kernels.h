@@ -798,27 +798,29 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 
     if constexpr (!(SYSID_EXP_SKIP & 4)) {  // diagnostics builds may skip this phase (J_c)
     // ---- contact Jacobian (LOCAL_WORLD_ALIGNED, linear rows) ----
-    for (int e = hl; e < k * nv; e += HW) {
-      const int rho = e / nv, r = e - rho * nv;
-      unsigned long long m = amask;  // the (rho/3)-th contact with a non-zero value
-      for (int t = rho / 3; t > 0; --t) m &= m - 1ull;
+    // lane = (contact in contact, dof): the three rows of the contact at once (one cross product)
+    for (int e = hl; e < na * nv; e += HW) {
+      const int ci = e / nv, r = e - ci * nv;
+      unsigned long long m = amask;  // the ci-th contact with a non-zero value
+      for (int t = ci; t > 0; --t) m &= m - 1ull;
       const int c = __ffsll((long long)m) - 1;
-      const int comp = rho - 3 * (rho / 3);
-      double val = 0.0;
+      double x[3] = {0.0, 0.0, 0.0};
       if ((csupp[c] >> r) & 1ull) {
         const double* W = Ws + 3 * r;
         if (jtype[dof_joint[r]] == JT_FREEFLYER && dof_k[r] < 3) {
-          val = W[comp];
+          x[0] = W[0]; x[1] = W[1]; x[2] = W[2];
         } else {
-          double d[3], x[3];
+          double d[3];
           d[0] = pfs[3 * c] - Pts[3 * r];
           d[1] = pfs[3 * c + 1] - Pts[3 * r + 1];
           d[2] = pfs[3 * c + 2] - Pts[3 * r + 2];
           cross3(W, d, x);
-          val = x[comp];
         }
       }
-      Jc[rho * nv + r] = val;
+      double* jr = Jc + 3 * ci * nv + r;
+      jr[0] = x[0];
+      jr[nv] = x[1];
+      jr[2 * nv] = x[2];
     }
     wsync();
 
