@@ -618,15 +618,59 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       wload[g * K2_WAVES + bw] += n;
       gload[g] += n;
     }
+    if (e->ngroups == 1) {
+      // One workgroup holds every super-tile: split off-diagonal super-tiles into row halves (two tiles each,
+      // sharing their A fragment; the skipped half rides in sp.y >> 8, k2_tile_skip) while free slots remain
+      // and the busiest SIMD gets lighter.  Spot: 15 super-tiles of 3-4 tiles, busiest SIMD 15 -> 14 tiles.
+      auto simd_max = [&](const std::vector<std::pair<int2, int>>& pcs, std::vector<int2>* out) {
+        std::vector<std::pair<int2, int>> v(pcs);
+        std::stable_sort(v.begin(), v.end(), [](const std::pair<int2, int>& a, const std::pair<int2, int>& b) {
+          return a.second > b.second;
+        });
+        std::vector<int> load(nsimd, 0), fill(nsimd, 0);
+        std::vector<int2> d((size_t)per_group, int2{-1, -1});
+        for (auto& pc : v) {
+          int b = -1;
+          for (int m = 0; m < nsimd; ++m)
+            if (fill[m] < wps * K2_SPW && (b < 0 || load[m] < load[b])) b = m;
+          if (b < 0) return 1 << 30;
+          const int slot = fill[b]++;  // SIMD b's slots: wave b + nsimd * (slot % wps), super slot slot / wps
+          d[(size_t)(b + nsimd * (slot % wps)) * K2_SPW + slot / wps] = pc.first;
+          load[b] += pc.second;
+        }
+        if (out) out->swap(d);
+        return *std::max_element(load.begin(), load.end());
+      };
+      std::vector<int> sload(nsimd, 0);
+      for (int w = 0; w < K2_WAVES; ++w) sload[w % nsimd] += wload[w];
+      int cur = *std::max_element(sload.begin(), sload.end());
+      std::vector<std::pair<int2, int>> pcs;
+      for (int2 t : order) pcs.push_back({t, ntiles(t)});
+      for (size_t x = 0; x < pcs.size() && (int)pcs.size() < per_group; ++x) {
+        const int2 t = pcs[x].first;
+        if (pcs[x].second != 4 || (t.y >> 8) != 0) continue;  // whole off-diagonal super-tiles only
+        std::vector<std::pair<int2, int>> trial(pcs);
+        trial[x] = {int2{t.x, t.y | (0xC << 8)}, 2};             // keep tiles 0, 1 (row 2 I0)
+        trial.push_back({int2{t.x, t.y | (0x3 << 8)}, 2});       // keep tiles 2, 3 (row 2 I0 + 1)
+        std::vector<int2> d;
+        const int m = simd_max(trial, &d);
+        if (m < cur) {
+          cur = m;
+          pcs.swap(trial);
+          dealt.swap(d);
+        }
+      }
+    }
     sl.swap(dealt);
   }
   std::vector<int2> tl(sl.size() * 4, int2{-1, -1});
   for (size_t k = 0; k < sl.size(); ++k) {
     if (sl[k].x < 0) continue;
+    const int skip = sl[k].y >> 8, sy = sl[k].y & 0xFF;
     for (int a = 0; a < 2; ++a)
       for (int b = 0; b < 2; ++b) {
-        const int I0 = 2 * sl[k].x + a, J0 = 2 * sl[k].y + b;
-        if (I0 <= J0 && I0 < e->ntc && J0 < e->ntc) tl[4 * k + 2 * a + b] = int2{I0, J0};
+        const int I0 = 2 * sl[k].x + a, J0 = 2 * sy + b;
+        if (I0 <= J0 && I0 < e->ntc && J0 < e->ntc && !((skip >> (2 * a + b)) & 1)) tl[4 * k + 2 * a + b] = int2{I0, J0};
       }
   }
   e->nslots = (int)tl.size();

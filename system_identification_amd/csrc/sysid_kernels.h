@@ -1419,6 +1419,10 @@ template <typename T> struct K2Acc;
 template <> struct K2Acc<double> { typedef dbl4 type; };
 template <> struct K2Acc<float> { typedef flt4 type; };
 
+// Super-tile slot descriptor {I0, J0 | skip << 8}: skip bit t drops tile t = 2a + b (a super-tile split into
+// row halves over two slots by the host's balancing; 0 otherwise).
+__device__ __forceinline__ bool k2_tile_skip(int2 sp, int t) { return sp.x >= 0 && ((sp.y >> (8 + t)) & 1); }
+
 __host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) / 32) * 32 + 16; }
 
 // Rows per staged chunk of the bf16 kernel: as many whole 32-row k-steps as two column-major LDS buffers of
@@ -1503,10 +1507,10 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int I = 2 * sp.x + (t >> 1), J = 2 * sp.y + (t & 1);
-      need[s][t] = live[s] && I <= J && J < NTC;
+      const int I = 2 * sp.x + (t >> 1), J = 2 * (sp.y & 0xFF) + (t & 1);
+      need[s][t] = live[s] && I <= J && J < NTC && !k2_tile_skip(sp, t);
     }
-    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
+    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * (sp.y & 0xFF), 2 * (sp.y & 0xFF) + 1};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
@@ -1713,10 +1717,10 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int I = 2 * sp.x + (t >> 1), J = 2 * sp.y + (t & 1);
-      need[s][t] = live[s] && I <= J && J < NTC;
+      const int I = 2 * sp.x + (t >> 1), J = 2 * (sp.y & 0xFF) + (t & 1);
+      need[s][t] = live[s] && I <= J && J < NTC && !k2_tile_skip(sp, t);
     }
-    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
+    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * (sp.y & 0xFF), 2 * (sp.y & 0xFF) + 1};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
@@ -1907,10 +1911,10 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int I = 2 * sp.x + (t >> 1), J = 2 * sp.y + (t & 1);
-      need[s][t] = live[s] && I <= J && J < NTC;
+      const int I = 2 * sp.x + (t >> 1), J = 2 * (sp.y & 0xFF) + (t & 1);
+      need[s][t] = live[s] && I <= J && J < NTC && !k2_tile_skip(sp, t);
     }
-    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * sp.y, 2 * sp.y + 1};
+    const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * (sp.y & 0xFF), 2 * (sp.y & 0xFF) + 1};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
