@@ -211,7 +211,7 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
               double* slab, hipStream_t st, int prec) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
-  const dim3 g2(e->ngroups * ks), b2(64 * K2_WAVES);
+  const dim3 g2(e->ngroups * ks), b2(64 * k2_waves(e->ntc));
   const double* p64 = static_cast<const double*>(d_panel);
   const float* p32 = static_cast<const float*>(d_panel);
   const __bf16* p16 = static_cast<const __bf16*>(d_panel);
@@ -239,7 +239,8 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
     } else if (prec == 1) {                                                                                 \
       SYSID_K2_F32(NTC, KC)                                                                                 \
     } else {                                                                                                \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, b2, 0, st, p16, rows, ld_panel,       \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16,   \
+                         rows, ld_panel,                                                                   \
                          e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                          \
     }                                                                                                       \
     break;
@@ -567,13 +568,14 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->k1_maxch_tpl = maxch_tpl;
 
   // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
-  // K2_WAVES x K2_SPW super slots per workgroup group; 4 tile slots per super slot.
+  // K2W x K2S super slots per workgroup group; 4 tile slots per super slot.
   e->ntc = (e->ncol + 15) / 16;
+  const int K2W = k2_waves(e->ntc), K2S = k2_spw(e->ntc);  // the K2 kernels' workgroup shape for this width
   const int nsg = (e->ntc + 1) / 2;
   std::vector<int2> sl;
   for (int I0 = 0; I0 < nsg; ++I0)
     for (int J0 = I0; J0 < nsg; ++J0) sl.push_back(int2{I0, J0});
-  const int per_group = K2_WAVES * K2_SPW;
+  const int per_group = K2W * K2S;
   e->ngroups = ((int)sl.size() + per_group - 1) / per_group;
   {
     // MFMA balance: super-tiles carry 1-4 tiles (diagonal ones skip their lower tile, edge ones the tiles
@@ -590,32 +592,32 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     };
     std::vector<int2> order(sl);
     std::stable_sort(order.begin(), order.end(), [&](int2 a, int2 b) { return ntiles(a) > ntiles(b); });
-    const int nsimd = 4, wps = K2_WAVES / nsimd;  // waves per SIMD
+    const int nsimd = 4, wps = K2W / nsimd;  // waves per SIMD
     std::vector<int2> dealt((size_t)e->ngroups * per_group, int2{-1, -1});
-    std::vector<int> gload(e->ngroups, 0), wload((size_t)e->ngroups * K2_WAVES, 0),
-        wfill((size_t)e->ngroups * K2_WAVES, 0);
+    std::vector<int> gload(e->ngroups, 0), wload((size_t)e->ngroups * K2W, 0),
+        wfill((size_t)e->ngroups * K2W, 0);
     for (int2 t : order) {
       const int n = ntiles(t);
       int g = -1;
       for (int x = 0; x < e->ngroups; ++x) {
         int free = 0;
-        for (int w = 0; w < K2_WAVES; ++w) free += K2_SPW - wfill[x * K2_WAVES + w];
+        for (int w = 0; w < K2W; ++w) free += K2S - wfill[x * K2W + w];
         if (free > 0 && (g < 0 || gload[x] < gload[g])) g = x;
       }
       int bw = -1;
-      for (int w = 0; w < K2_WAVES; ++w) {
-        if (wfill[g * K2_WAVES + w] >= K2_SPW) continue;
+      for (int w = 0; w < K2W; ++w) {
+        if (wfill[g * K2W + w] >= K2S) continue;
         const int sm = w % nsimd;
         int sl_load = 0;
-        for (int k = 0; k < wps; ++k) sl_load += wload[g * K2_WAVES + sm + nsimd * k];
+        for (int k = 0; k < wps; ++k) sl_load += wload[g * K2W + sm + nsimd * k];
         int bl = 0;
         if (bw >= 0)
-          for (int k = 0; k < wps; ++k) bl += wload[g * K2_WAVES + bw % nsimd + nsimd * k];
-        if (bw < 0 || sl_load < bl || (sl_load == bl && wload[g * K2_WAVES + w] < wload[g * K2_WAVES + bw])) bw = w;
+          for (int k = 0; k < wps; ++k) bl += wload[g * K2W + bw % nsimd + nsimd * k];
+        if (bw < 0 || sl_load < bl || (sl_load == bl && wload[g * K2W + w] < wload[g * K2W + bw])) bw = w;
       }
-      dealt[(size_t)(g * K2_WAVES + bw) * K2_SPW + wfill[g * K2_WAVES + bw]] = t;
-      ++wfill[g * K2_WAVES + bw];
-      wload[g * K2_WAVES + bw] += n;
+      dealt[(size_t)(g * K2W + bw) * K2S + wfill[g * K2W + bw]] = t;
+      ++wfill[g * K2W + bw];
+      wload[g * K2W + bw] += n;
       gload[g] += n;
     }
     if (e->ngroups == 1) {
@@ -632,17 +634,17 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
         for (auto& pc : v) {
           int b = -1;
           for (int m = 0; m < nsimd; ++m)
-            if (fill[m] < wps * K2_SPW && (b < 0 || load[m] < load[b])) b = m;
+            if (fill[m] < wps * K2S && (b < 0 || load[m] < load[b])) b = m;
           if (b < 0) return 1 << 30;
           const int slot = fill[b]++;  // SIMD b's slots: wave b + nsimd * (slot % wps), super slot slot / wps
-          d[(size_t)(b + nsimd * (slot % wps)) * K2_SPW + slot / wps] = pc.first;
+          d[(size_t)(b + nsimd * (slot % wps)) * K2S + slot / wps] = pc.first;
           load[b] += pc.second;
         }
         if (out) out->swap(d);
         return *std::max_element(load.begin(), load.end());
       };
       std::vector<int> sload(nsimd, 0);
-      for (int w = 0; w < K2_WAVES; ++w) sload[w % nsimd] += wload[w];
+      for (int w = 0; w < K2W; ++w) sload[w % nsimd] += wload[w];
       int cur = *std::max_element(sload.begin(), sload.end());
       std::vector<std::pair<int2, int>> pcs;
       for (int2 t : order) pcs.push_back({t, ntiles(t)});

@@ -20,7 +20,6 @@ namespace sysid_dev {
 constexpr int JT_FREEFLYER = 1;
 constexpr int JT_REVOLUTE = 2;
 constexpr int K1_WAVES = 4;            // waves (= samples in flight) per K1 workgroup
-constexpr int K2_WAVES = 8;            // waves per K2 workgroup
 constexpr int K1_SHARDS = 8;           // K1 sample ranges / claim counters (one per XCD), 128 B apart
 
 // ------------------------------------------------------------------------------------------------
@@ -1390,13 +1389,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 // ------------------------------------------------------------------------------------------------
 // K2: G_partial[ks] = panel[rows of ks]^T panel[rows of ks]   (fp64 MFMA 16x16x4, upper tiles)
 //
-// Each workgroup (K2_WAVES waves) walks a contiguous row range in chunks of KC rows.  A chunk of the
+// Each workgroup (k2_waves(NTC) waves) walks a contiguous row range in chunks of KC rows.  A chunk of the
 // panel is one contiguous byte range in HBM; every thread copies fixed double2 slots of it (offsets
 // computed once, no divisions in the loop) through registers into an LDS buffer with a padded row
 // stride (STRIDE ≡ 16 mod 32 doubles, so the 2 rows x 16 doubles of a 32-lane ds_read_b64 group hit
 // disjoint banks).  Two LDS buffers and two staging register sets: chunk c+2's global loads are in flight
 // while chunk c is multiplied and chunk c+1 is written to LDS.
-// Each wave owns K2_SPW "super-tiles" (2x2 blocks of 16x16 output tiles): 4 fragment reads feed 4 MFMAs.
+// Each wave owns k2_spw(NTC) "super-tiles" (2x2 blocks of 16x16 output tiles): 4 fragment reads feed 4 MFMAs.
 // The k-loop over a chunk is fully unrolled, so fragment reads use immediate LDS offsets.
 // Fragment = 16 consecutive doubles of 4 consecutive rows: lane l holds row (l>>4), col (l&15), which is
 // both the A layout (A[i=l&15][k=l>>4]) and the B layout (B[k=l>>4][j=l&15]) of v_mfma_f64_16x16x4_f64.
@@ -1404,7 +1403,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef float flt4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int K2_SPW = 2;   // super-tiles per wave
+// Waves per K2 workgroup and super-tile slots per wave, by Gram width: narrow Grams (one workgroup holds every
+// super-tile, Spot: 16 pieces) run 16 waves of one slot each -- four waves per SIMD hide the per-chunk barrier
+// and fragment-read latency better than two waves of two slots (Spot K2 -3.9%, profiles/r02_ab2/k2_waves16_ab.txt);
+// wide ones 8 waves of two slots (the LDS-DMA kernel deals its chunk rows to 8 waves).
+__host__ __device__ constexpr int k2_waves(int ntc) { return ntc < 16 ? 16 : 8; }
+__host__ __device__ constexpr int k2_spw(int ntc) { return ntc < 16 ? 1 : 2; }
+constexpr int K2_BF16_WAVES = 8;  // the bf16 kernel's waves (it takes k2_waves * k2_spw / 8 slots per wave)
 #ifndef SYSID_K2_UNIFORM
 #define SYSID_K2_UNIFORM 0  // readfirstlane'd descriptors measured slower (G1 K2 1.80 -> 2.26 ms, Spot +3%)
 #endif
@@ -1436,13 +1441,14 @@ __host__ __device__ constexpr int k2_bf16_kc(int ntc) {
 }
 
 template <typename T, int NTC, int KC>
-__global__ void __launch_bounds__(64 * K2_WAVES)
+__global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
              int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   typedef typename K2Acc<T>::type accT;
+  constexpr int K2W = k2_waves(NTC), K2S = k2_spw(NTC);
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;                       // elements per LDS buffer
-  constexpr int NT = 64 * K2_WAVES;
+  constexpr int NT = 64 * K2W;
   __shared__ T lds[2 * BUF];
   const int group = blockIdx.x % ngroups;
   const int ks = blockIdx.x / ngroups;
@@ -1451,7 +1457,7 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   const int64_t r0 = (nck * ks / ksplit) * KC;
   const int64_t r1 = ks + 1 == ksplit ? rows : (nck * (ks + 1) / ksplit) * KC;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sbase = (group * K2_WAVES + wave) * K2_SPW;
+  const int sbase = (group * K2W + wave) * K2S;
 
   // zero both buffers once: columns >= ldp (up to NTC*16) are never staged and must read as 0
   for (int x = threadIdx.x; x < 2 * BUF; x += NT) lds[x] = 0.0;
@@ -1492,11 +1498,11 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   };
 
   // fragment columns of this wave: f = 4*s + {I0, I0+1, J0, J0+1} (16-column blocks)
-  int foff[4 * K2_SPW];
-  bool live[K2_SPW];
-  bool need[K2_SPW][4];  // wave-uniform: skip the lower tile of a diagonal super-tile, tiles past NTC
+  int foff[4 * K2S];
+  bool live[K2S];
+  bool need[K2S][4];  // wave-uniform: skip the lower tile of a diagonal super-tile, tiles past NTC
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s) {
+  for (int s = 0; s < K2S; ++s) {
     int2 sp = supers[sbase + s];
 #if SYSID_K2_UNIFORM
     // wave-uniform by construction (sbase depends on the wave only): SGPRs, so the tile tests below are
@@ -1517,9 +1523,9 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
       foff[4 * s + u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
     }
   }
-  accT acc[K2_SPW][4];
+  accT acc[K2S][4];
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s)
+  for (int s = 0; s < K2S; ++s)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
 
@@ -1532,11 +1538,11 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   auto mfma_chunk = [&](const T* cur) {
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
-      T x[4 * K2_SPW];
+      T x[4 * K2S];
 #pragma unroll
-      for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = cur[foff[u] + kk * STRIDE];
+      for (int u = 0; u < 4 * K2S; ++u) x[u] = cur[foff[u] + kk * STRIDE];
 #pragma unroll
-      for (int s = 0; s < K2_SPW; ++s) {
+      for (int s = 0; s < K2S; ++s) {
         constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1604,7 +1610,7 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   }
   // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s) {
+  for (int s = 0; s < K2S; ++s) {
     if (!live[s]) continue;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1661,15 +1667,16 @@ __host__ __device__ constexpr int k2_dma_kc(int ntc) {
 }
 
 template <typename T, int NTC, int KC>
-__global__ void __launch_bounds__(64 * K2_WAVES)
+__global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
                  int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   typedef typename K2Acc<T>::type accT;
-  static_assert(KC % K2_WAVES == 0 && KC % 4 == 0, "chunk rows are dealt to the 8 waves, k-steps of 4");
+  constexpr int K2W = k2_waves(NTC), K2S = k2_spw(NTC);
+  static_assert(KC % K2W == 0 && KC % 4 == 0, "chunk rows are dealt to the waves, k-steps of 4");
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;  // elements per LDS buffer
-  constexpr int NT = 64 * K2_WAVES;
-  constexpr int RPW = KC / K2_WAVES;  // rows per wave per chunk
+  constexpr int NT = 64 * K2W;
+  constexpr int RPW = KC / K2W;  // rows per wave per chunk
   constexpr int EB = (int)sizeof(T);
   static_assert(3 * BUF * EB <= 160 * 1024, "three LDS buffers");
   __shared__ __attribute__((aligned(16))) T lds[3 * BUF];
@@ -1679,7 +1686,7 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   const int64_t r0 = 4 * (q4 * ks / ksplit);
   const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sbase = (group * K2_WAVES + wave) * K2_SPW;
+  const int sbase = (group * K2W + wave) * K2S;
 
   // zero the three buffers once: columns >= ldp (up to NTC*16) are never written by the DMA and must read as 0
   for (int x = threadIdx.x; x < 3 * BUF; x += NT) lds[x] = (T)0;
@@ -1703,16 +1710,16 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   auto dma_chunk = [&](int64_t c0, T* buf) {  // RPW * np instructions per wave
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-      const int rr = wave + K2_WAVES * q;
+      const int rr = wave + K2W * q;
       dma_row(panel + (c0 + rr) * ldp, buf + rr * STRIDE);
     }
   };
 
-  int foff[4 * K2_SPW];
-  bool live[K2_SPW];
-  bool need[K2_SPW][4];
+  int foff[4 * K2S];
+  bool live[K2S];
+  bool need[K2S][4];
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s) {
+  for (int s = 0; s < K2S; ++s) {
     int2 sp = supers[sbase + s];
     live[s] = sp.x >= 0;
 #pragma unroll
@@ -1727,19 +1734,19 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
       foff[4 * s + u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
     }
   }
-  accT acc[K2_SPW][4];
+  accT acc[K2S][4];
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s)
+  for (int s = 0; s < K2S; ++s)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
   auto mfma_chunk = [&](const T* cur) {
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
-      T x[4 * K2_SPW];
+      T x[4 * K2S];
 #pragma unroll
-      for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = cur[foff[u] + kk * STRIDE];
+      for (int u = 0; u < 4 * K2S; ++u) x[u] = cur[foff[u] + kk * STRIDE];
 #pragma unroll
-      for (int s = 0; s < K2_SPW; ++s) {
+      for (int s = 0; s < K2S; ++s) {
         constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1783,7 +1790,7 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
     const int valid = (int)(r1 - c0);
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-      const int rr = wave + K2_WAVES * q;
+      const int rr = wave + K2W * q;
       T* dst = b0 + rr * STRIDE;
       if (rr < valid) {
         dma_row(panel + (c0 + rr) * ldp, dst);
@@ -1797,7 +1804,7 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   }
   // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s) {
+  for (int s = 0; s < K2S; ++s) {
     if (!live[s]) continue;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1843,14 +1850,16 @@ __device__ __forceinline__ void transpose8x8_b16(const uint4 (&in)[8], uint4 (&o
 }
 
 template <int NTC, int KC>
-__global__ void __launch_bounds__(64 * K2_WAVES)
+__global__ void __launch_bounds__(64 * K2_BF16_WAVES)
 k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
                   int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   static_assert(KC % 32 == 0, "bf16 K2 chunks are whole 32-row k-steps");
+  // always 8 waves (16 spill its transposes at 128 VGPRs), over the same slots per group as the f64 kernels
+  constexpr int K2W = K2_BF16_WAVES, K2S = k2_waves(NTC) * k2_spw(NTC) / K2_BF16_WAVES;
   constexpr int NCOL = NTC * 16;
   constexpr int CS = KC + 8;
   constexpr int BUF = NCOL * CS;
-  constexpr int NT = 64 * K2_WAVES;
+  constexpr int NT = 64 * K2W;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
   const int group = blockIdx.x % ngroups;
   const int ks = blockIdx.x / ngroups;
@@ -1858,7 +1867,7 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
   const int64_t r0 = 4 * (q4 * ks / ksplit);
   const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sbase = (group * K2_WAVES + wave) * K2_SPW;
+  const int sbase = (group * K2W + wave) * K2S;
 
   // zero both buffers once: columns >= ldp are never staged and must read as 0
   for (int x = threadIdx.x; x < 2 * BUF; x += NT) lds[x] = (__bf16)0.0f;
@@ -1896,11 +1905,11 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
     }
   };
 
-  int foff[4 * K2_SPW];
-  bool live[K2_SPW];
-  bool need[K2_SPW][4];
+  int foff[4 * K2S];
+  bool live[K2S];
+  bool need[K2S][4];
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s) {
+  for (int s = 0; s < K2S; ++s) {
     int2 sp = supers[sbase + s];
 #if SYSID_K2_UNIFORM
     // wave-uniform by construction (sbase depends on the wave only): SGPRs, so the tile tests below are
@@ -1921,9 +1930,9 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
       foff[4 * s + u] = (16 * b + (lane & 15)) * CS + 8 * (lane >> 4);
     }
   }
-  flt4 acc[K2_SPW][4];
+  flt4 acc[K2S][4];
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s)
+  for (int s = 0; s < K2S; ++s)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[s][t] = flt4{0.f, 0.f, 0.f, 0.f};
 
@@ -1939,11 +1948,11 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
     if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * KC);
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 32) {
-      bf16x8 x[4 * K2_SPW];
+      bf16x8 x[4 * K2S];
 #pragma unroll
-      for (int u = 0; u < 4 * K2_SPW; ++u) x[u] = *reinterpret_cast<const bf16x8*>(cur + foff[u] + kk);
+      for (int u = 0; u < 4 * K2S; ++u) x[u] = *reinterpret_cast<const bf16x8*>(cur + foff[u] + kk);
 #pragma unroll
-      for (int s = 0; s < K2_SPW; ++s) {
+      for (int s = 0; s < K2S; ++s) {
         constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1956,7 +1965,7 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
     __syncthreads();
   }
 #pragma unroll
-  for (int s = 0; s < K2_SPW; ++s) {
+  for (int s = 0; s < K2S; ++s) {
     if (!live[s]) continue;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
