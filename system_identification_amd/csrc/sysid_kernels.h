@@ -824,8 +824,10 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
 
     }
-    // H1 computed with P by the register-blocked quadruped path (free-flyer dofs 0..5)
-    const bool h1_fused = NVC == 18 && HW == 32 && kp.has_ff && kp.ff0 == 0;
+    // H1 = P[:, ff] J_w[:, ff]^T is P's free-flyer columns: in base coordinates the free-flyer's motion axes
+    // are the unit vectors (oR = I, ot = 0), J_w[:, ff] = I exactly.  The column phase reads those P entries
+    // in place (an even ff0 keeps the rows' 16-byte alignment); otherwise H1 is copied out below.
+    const bool h1_in_p = kp.has_ff && (kp.ff0 & 1) == 0;
     if (kp.full) {
       // get_full_regressor_force (src/sys_identification.py:391-399): no projection
       for (int e = hl; e < nv * nv; e += HW) {
@@ -987,9 +989,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       // ---- P = I - Q^T Q  (Zt row a = column a of Q; J_c rows = rows of Q) ----
       if constexpr (NVC == 18 && HW == 32) {
         // Register-blocked: lane = (row pair, 6-column group), 27 lanes x 12 entries, every load before
-        // any store, so P may overwrite Zt freely and no ordering point is needed between entries.  The
-        // lanes of column group 0 hold P[a, 0:6] and also write H1 = P[:, ff] J_w[:, ff]^T for their two
-        // rows (over J_c, read completely by then) when the free-flyer's dofs are 0..5.
+        // any store, so P may overwrite Zt freely and no ordering point is needed between entries.
         const int rp = hl / 3, cg = hl - 3 * rp;
         if (hl < 27) {
           const int a0 = 2 * rp, b0 = 6 * cg;
@@ -1016,36 +1016,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int c = 0; c < 6; ++c) pv[i][c] = (a0 + i == b0 + c ? 1.0 : 0.0) - acc[i][c];
-          const bool h1_here = cg == 0 && h1_fused;
-          double h[2][6];
-          if (h1_here) {
-#pragma unroll
-            for (int c = 0; c < 6; ++c) {
-              double j6[6];
-#pragma unroll
-              for (int d = 0; d < 6; ++d) j6[d] = Jws[6 * d + c];
-#pragma unroll
-              for (int i = 0; i < 2; ++i) {
-                double x = 0.0;
-#pragma unroll
-                for (int d = 0; d < 6; ++d) x += pv[i][d] * j6[d];
-                h[i][c] = x;
-              }
-            }
-          }
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             double2* pr = reinterpret_cast<double2*>(Ps + (a0 + i) * 18 + b0);
 #pragma unroll
             for (int c = 0; c < 3; ++c) pr[c] = make_double2(pv[i][2 * c], pv[i][2 * c + 1]);
-          }
-          if (h1_here) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              double2* hr = reinterpret_cast<double2*>(H1 + (a0 + i) * 6);
-#pragma unroll
-              for (int c = 0; c < 3; ++c) hr[c] = make_double2(h[i][2 * c], h[i][2 * c + 1]);
-            }
           }
         }
         wsync();
@@ -1099,12 +1074,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       tps[r] = acc;
     }
     if (kp.full) wsync();
-    for (int e = hl; e < nv * 6 && !(h1_fused && !kp.full); e += HW) {
+    for (int e = hl; e < nv * 6 && !h1_in_p; e += HW) {
       const int r = e / 6, c = e - 6 * r;
-      double h = 0.0;
-      if (kp.has_ff)
-        for (int d = 0; d < 6; ++d) h += Ps[r * nv + kp.ff0 + d] * Jws[6 * (kp.ff0 + d) + c];
-      H1[e] = h;
+      H1[e] = kp.has_ff ? Ps[r * nv + kp.ff0 + c] : 0.0;  // J_w[:, ff] = I (see h1_in_p)
     }
     wsync();
     }
@@ -1133,7 +1105,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     OutT* out = panel + ((s + half) * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
     auto block_row = [&](int r, const double* F, const int* dof, int cl, double* y) {
-      const double* h = H1 + 6 * r;
+      const double* h = h1_in_p ? Ps + r * nv + kp.ff0 : H1 + 6 * r;
       const double* pr = Ps + r * nv;
       double G[6];
 #pragma unroll
@@ -1204,7 +1176,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         for (int k = 0; k < 6; ++k) jw[t][k] = t < cl ? Jws[6 * dof[t] + k] : 0.0;
       double hn[6], pn[MAXCH];
       auto row_load = [&](int r, double* h, double* pp) {
-        const double2* h2 = reinterpret_cast<const double2*>(H1 + 6 * r);
+        const double2* h2 = reinterpret_cast<const double2*>(h1_in_p ? Ps + r * NVC + kp.ff0 : H1 + 6 * r);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const double2 v = h2[k];
