@@ -642,48 +642,37 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // pinocchio only see the base rotation through R_b^T g, and J_c's row space (hence P) is the same in
     // base-aligned and world-aligned axes because R_b is invertible.  This stays exact for the float32,
     // slightly non-unit quaternions of the reference's .dat logs.
-    auto pose_step = [&](int j) {
+    auto pose_step = [&](int j) {  // depth >= 2: a revolute joint (the free-flyer is on the first level)
       const double* bp = body + BODY_STRIDE * parent[j];
       double* bj = body + BODY_STRIDE * j;
-      double oR[9], ot[3];
-      if (jtype[j] == JT_FREEFLYER) {
-        oR[0] = 1.0; oR[1] = 0.0; oR[2] = 0.0; oR[3] = 0.0; oR[4] = 1.0; oR[5] = 0.0;
-        oR[6] = 0.0; oR[7] = 0.0; oR[8] = 1.0;
-        ot[0] = ot[1] = ot[2] = 0.0;
-      } else {
-        double liR[9], lit[3];
+      double liR[9], lit[3], oR[9], ot[3];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) liR[k] = bj[k];
-        lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
-        mat3mul(bp, liR, oR);
-        mat3vec(bp, lit, ot);
-        ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
-      }
+      for (int k = 0; k < 9; ++k) liR[k] = bj[k];
+      lit[0] = bj[9]; lit[1] = bj[10]; lit[2] = bj[11];
+      mat3mul(bp, liR, oR);
+      mat3vec(bp, lit, ot);
+      ot[0] += bp[9]; ot[1] += bp[10]; ot[2] += bp[11];
 #pragma unroll
       for (int k = 0; k < 9; ++k) bj[k] = oR[k];
       bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];
     };
     if constexpr (!(SYSID_EXP_SKIP & 1)) {  // diagnostics builds may skip this phase (forward kinematics)
     for (int j = 1 + hl; j < NJ; j += HW) {
-      const int iq = idx_q[j];
-      double RJ[9], tJ[3];
-      if (jtype[j] == JT_FREEFLYER) {
-        quat_to_matrix(q[iq + 3], q[iq + 4], q[iq + 5], q[iq + 6], RJ);
-        tJ[0] = q[iq]; tJ[1] = q[iq + 1]; tJ[2] = q[iq + 2];
-      } else {
-        axis_rotation(axis + 3 * j, q[iq], RJ);
-        tJ[0] = tJ[1] = tJ[2] = 0.0;
-      }
       double* bj = body + BODY_STRIDE * j;
-      double tmp[3];
-      mat3mul(R0 + 9 * j, RJ, bj);
-      mat3vec(R0 + 9 * j, tJ, tmp);
-      bj[9] = tmp[0] + t0[3 * j]; bj[10] = tmp[1] + t0[3 * j + 1]; bj[11] = tmp[2] + t0[3 * j + 2];
-      if (depth[j] == 1) pose_step(j);
+      if (jtype[j] == JT_FREEFLYER) {
+        // its pose in its own (base) frame: I, 0 (the quaternion only enters through R_b^T g, in part (2))
+#pragma unroll
+        for (int k = 0; k < 12; ++k) bj[k] = (k == 0 || k == 4 || k == 8) ? 1.0 : 0.0;
+      } else {
+        // liMi = (R0 R_axis(q), t0); on the first level (parent = the universe) that is the pose itself
+        double RJ[9];
+        axis_rotation(axis + 3 * j, q[idx_q[j]], RJ);
+        mat3mul(R0 + 9 * j, RJ, bj);
+        bj[9] = t0[3 * j]; bj[10] = t0[3 * j + 1]; bj[11] = t0[3 * j + 2];
+      }
     }
     wsync();
-    // Poses level by level (a joint's parent is one level up); level 1 (parent = the universe, whose
-    // record is set at the top of the step) runs in the placement pass.
+    // Poses level by level (a joint's parent is one level up); level 1 is final after the placement pass.
     for (int lvl = 2; lvl <= kp.maxdepth; ++lvl) {
       for (int j = 1 + hl; j < NJ; j += HW)
         if (depth[j] == lvl) pose_step(j);
