@@ -747,7 +747,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         V[0] = V[1] = V[2] = V[3] = V[4] = V[5] = A[3] = A[4] = A[5] = 0.0;
       }
       const int* ch = chain + j * kp.maxch;
-      for (int t = 0; t < cl; ++t) {
+#pragma unroll
+      for (int t = 0; t < MAXCH; ++t) {  // unrolled to the compile-time chain slots (K1 -1.3%)
+        if (t >= cl) break;
         const int d = ch[t];
         const double* S = Jws + 6 * d;
         const double qd = dq[d], qdd = ddq[d];
