@@ -1185,10 +1185,60 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #ifndef SYSID_K1_YST_SBASE
 #define SYSID_K1_YST_SBASE 1
 #endif
+#ifndef SYSID_K1_YPP
+#define SYSID_K1_YPP 1
+#endif
 #if SYSID_K1_YST_SBASE
       char* ybase = reinterpret_cast<char*>(panel + (s * NVC) * ldp);
       const uint32_t yhoff = (uint32_t)(half * NVC * (int)ldp * (int)sizeof(OutT));
 #endif
+#if SYSID_K1_YPP && SYSID_K1_COLV >= 2 && !defined(SYSID_EXP_NO_YCOMP)
+      // Rows in pairs with two explicit H1 / P register sets (no copies between them): row rho + 1's LDS reads
+      // are in flight while row rho is multiplied, staged and stored.  The P entries past the body's chain
+      // (dof slot 0, a finite entry of P) meet zero motion axes (jw), so they add exact zeros: no mask.
+      double hB[6], pB[MAXCH];
+      auto yrow = [&](int rho, const double* hc, const double* pc) {
+        if (act) {
+          double y[10], G[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) G[k] = hc[k];
+#pragma unroll
+          for (int t = 0; t < MAXCH; ++t)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) G[k] += pc[t] * jw[t][k];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            y[c] = G[0] * F[6 * c] + G[1] * F[6 * c + 1] + G[2] * F[6 * c + 2] + G[3] * F[6 * c + 3] +
+                   G[4] * F[6 * c + 4] + G[5] * F[6 * c + 5];
+#pragma unroll
+          for (int c = 0; c < 6; ++c)
+            y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
+          double2* sp = reinterpret_cast<double2*>(stg + g * kp.wy + 10 * (i - 1));
+#pragma unroll
+          for (int c = 0; c < 5; ++c) sp[c] = make_double2(y[2 * c], y[2 * c + 1]);
+        }
+        wsync();
+        if (valid) {
+          const double2* s2 = reinterpret_cast<const double2*>(stg);
+          const int dg = RH * (int)ldp - kp.wy;
+          char* rb = ybase + (int64_t)rho * ldp * (int64_t)sizeof(OutT);
+          for (int x = hl; x < n2; x += HW) {
+            const uint32_t off = yhoff + (uint32_t)((2 * x + (x >= wy2 ? dg : 0)) * (int)sizeof(OutT));
+            panel_store(reinterpret_cast<OutT*>(rb + off), s2[x].x, s2[x].y);
+          }
+        }
+        wsync();
+      };
+      int rho = 0;
+#pragma unroll 1
+      for (; rho + 1 < RH; rho += 2) {
+        row_load(g * RH + rho + 1, hB, pB);
+        yrow(rho, hn, pn);
+        if (rho + 2 < RH) row_load(g * RH + rho + 2, hn, pn);
+        yrow(rho + 1, hB, pB);
+      }
+      if (rho < RH) yrow(rho, hn, pn);
+#else
 #pragma unroll 1
       for (int rho = 0; rho < RH; ++rho) {
         if (act) {
@@ -1251,6 +1301,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
         wsync();
       }
+#endif
     } else {
       for (int it = hl; it < nyi && valid; it += HW) {
         const int g = it / nbody, i = it - g * nbody + 1;
