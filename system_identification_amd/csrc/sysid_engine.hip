@@ -53,6 +53,8 @@ struct sysid_engine {
   // K2/K3 Gram tiling
   int ntc = 0, nslots = 0, nsuper = 0, ngroups = 0;
   int2* d_tiles = nullptr;
+  int nslots_b = 0, nsuper_b = 0, ngroups_b = 0;  // the bf16 kernel's deal (k2_bf16_spw slots per wave)
+  int2* d_tiles_b = nullptr;
   // host-API buffers (grow-only)
   double* d_in = nullptr;
   size_t in_cap = 0;
@@ -96,13 +98,14 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
   // the bf16 kernel's large chunks take most of a CU's LDS: one workgroup per CU
   const int mult = (e->ntc >= 16 || (SYSID_K2_DMA_NARROW && e->ntc <= 10)) && prec != 2 ? 2 : 1;
-  int ks = std::max(1, mult * e->cus / std::max(1, e->ngroups));
+  int ks = std::max(1, mult * e->cus / std::max(1, prec == 2 ? e->ngroups_b : e->ngroups));
   const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
 }
 
-size_t slab_bytes(const sysid_engine* e, int64_t rows) {
-  return align256((size_t)ksplit_for(e, rows) * e->nslots * 256 * sizeof(double));
+size_t slab_bytes(const sysid_engine* e, int64_t rows, int prec = 0) {
+  const int nslots = prec == 2 ? e->nslots_b : e->nslots;
+  return align256((size_t)ksplit_for(e, rows, prec) * nslots * 256 * sizeof(double));
 }
 
 int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
@@ -239,9 +242,9 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
     } else if (prec == 1) {                                                                                 \
       SYSID_K2_F32(NTC, KC)                                                                                 \
     } else {                                                                                                \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16,   \
-                         rows, ld_panel,                                                                   \
-                         e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                          \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), dim3(e->ngroups_b * ks),                  \
+                         dim3(64 * K2_BF16_WAVES), 0, st, p16, rows, ld_panel,                              \
+                         e->d_tiles_b, e->ngroups_b, ks, e->nslots_b, accumulate, slab);                    \
     }                                                                                                       \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
@@ -258,10 +261,12 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
   return SYSID_OK;
 }
 
-int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st) {
-  const int64_t nx = (int64_t)e->nslots * 256;
-  hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, e->d_tiles + e->nsuper, nx,
-                     ks, e->ncol, d_gram);
+int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st, int prec = 0) {
+  const bool b = prec == 2;  // the bf16 kernel's slabs follow its own deal
+  const int64_t nx = (int64_t)(b ? e->nslots_b : e->nslots) * 256;
+  const int2* tiles = b ? e->d_tiles_b + e->nsuper_b : e->d_tiles + e->nsuper;
+  hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, tiles, nx, ks, e->ncol,
+                     d_gram);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
@@ -341,7 +346,7 @@ int64_t gram_chunk(const sysid_engine* e, int64_t N, int prec) {
 // [K1 counter | panel chunk | K2 slabs]
 size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
   const int64_t rows = gram_chunk(e, N, prec) * e->nv;
-  return WORK_BYTES + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) + slab_bytes(e, rows);
+  return WORK_BYTES + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) + slab_bytes(e, rows, prec);
 }
 
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
@@ -361,7 +366,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   auto* work = static_cast<unsigned long long*>(d_ws);
   char* panel = static_cast<char*>(d_ws) + WORK_BYTES;
   double* slab = reinterpret_cast<double*>(panel + align256((size_t)rows0 * ldc * prec_bytes(prec)));
-  const int ks0 = ksplit_for(e, rows0, prec);  // <= ksplit_for(e, rows0): the slabs fit the workspace
+  const int ks0 = ksplit_for(e, rows0, prec);  // slab_bytes(e, rows0, prec): the slabs fit the workspace
   int rc;
   size_t k = 0;
   auto mark = [&]() -> int {
@@ -376,7 +381,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     if ((rc = launch_k2(e, panel, n * e->nv, ldc, ks, c0 > 0, slab, st, prec)) != SYSID_OK) return rc;
   }
   if ((rc = mark())) return rc;
-  if ((rc = launch_k3(e, ks0, slab, d_gram, st))) return rc;
+  if ((rc = launch_k3(e, ks0, slab, d_gram, st, prec))) return rc;
   return mark();
 }
 
@@ -570,115 +575,121 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
   // K2W x K2S super slots per workgroup group; 4 tile slots per super slot.
   e->ntc = (e->ncol + 15) / 16;
-  const int K2W = k2_waves(e->ntc), K2S = k2_spw(e->ntc);  // the K2 kernels' workgroup shape for this width
-  const int nsg = (e->ntc + 1) / 2;
-  std::vector<int2> sl;
-  for (int I0 = 0; I0 < nsg; ++I0)
-    for (int J0 = I0; J0 < nsg; ++J0) sl.push_back(int2{I0, J0});
-  const int per_group = K2W * K2S;
-  e->ngroups = ((int)sl.size() + per_group - 1) / per_group;
-  {
-    // MFMA balance: super-tiles carry 1-4 tiles (diagonal ones skip their lower tile, edge ones the tiles
-    // past the Gram).  The waves of a workgroup share 4 SIMDs (wave w on SIMD w % 4, two waves each), so
-    // super-tiles are dealt largest first to the least loaded group, then SIMD, then wave with a free slot.
-    auto ntiles = [&](int2 t) {
-      int n = 0;
+  // K2W waves x K2S super slots per workgroup group -> d_tiles = [super slots | tile slots]
+  auto deal = [&](int K2W, int K2S, int& ngroups, int& nsuper, int& nslots) -> std::vector<int2> {
+    const int nsg = (e->ntc + 1) / 2;
+    std::vector<int2> sl;
+    for (int I0 = 0; I0 < nsg; ++I0)
+      for (int J0 = I0; J0 < nsg; ++J0) sl.push_back(int2{I0, J0});
+    const int per_group = K2W * K2S;
+    ngroups = ((int)sl.size() + per_group - 1) / per_group;
+    {
+      // MFMA balance: super-tiles carry 1-4 tiles (diagonal ones skip their lower tile, edge ones the tiles
+      // past the Gram).  The waves of a workgroup share 4 SIMDs (wave w on SIMD w % 4, two waves each), so
+      // super-tiles are dealt largest first to the least loaded group, then SIMD, then wave with a free slot.
+      auto ntiles = [&](int2 t) {
+        int n = 0;
+        for (int a = 0; a < 2; ++a)
+          for (int b = 0; b < 2; ++b) {
+            const int I0 = 2 * t.x + a, J0 = 2 * t.y + b;
+            n += (I0 <= J0 && J0 < e->ntc) ? 1 : 0;
+          }
+        return n;
+      };
+      std::vector<int2> order(sl);
+      std::stable_sort(order.begin(), order.end(), [&](int2 a, int2 b) { return ntiles(a) > ntiles(b); });
+      const int nsimd = 4, wps = K2W / nsimd;  // waves per SIMD
+      std::vector<int2> dealt((size_t)ngroups * per_group, int2{-1, -1});
+      std::vector<int> gload(ngroups, 0), wload((size_t)ngroups * K2W, 0),
+          wfill((size_t)ngroups * K2W, 0);
+      for (int2 t : order) {
+        const int n = ntiles(t);
+        int g = -1;
+        for (int x = 0; x < ngroups; ++x) {
+          int free = 0;
+          for (int w = 0; w < K2W; ++w) free += K2S - wfill[x * K2W + w];
+          if (free > 0 && (g < 0 || gload[x] < gload[g])) g = x;
+        }
+        int bw = -1;
+        for (int w = 0; w < K2W; ++w) {
+          if (wfill[g * K2W + w] >= K2S) continue;
+          const int sm = w % nsimd;
+          int sl_load = 0;
+          for (int k = 0; k < wps; ++k) sl_load += wload[g * K2W + sm + nsimd * k];
+          int bl = 0;
+          if (bw >= 0)
+            for (int k = 0; k < wps; ++k) bl += wload[g * K2W + bw % nsimd + nsimd * k];
+          if (bw < 0 || sl_load < bl || (sl_load == bl && wload[g * K2W + w] < wload[g * K2W + bw])) bw = w;
+        }
+        dealt[(size_t)(g * K2W + bw) * K2S + wfill[g * K2W + bw]] = t;
+        ++wfill[g * K2W + bw];
+        wload[g * K2W + bw] += n;
+        gload[g] += n;
+      }
+      if (ngroups == 1) {
+        // One workgroup holds every super-tile: split off-diagonal super-tiles into row halves (two tiles each,
+        // sharing their A fragment; the skipped half rides in sp.y >> 8, k2_tile_skip) while free slots remain
+        // and the busiest SIMD gets lighter.  Spot: 15 super-tiles of 3-4 tiles, busiest SIMD 15 -> 14 tiles.
+        auto simd_max = [&](const std::vector<std::pair<int2, int>>& pcs, std::vector<int2>* out) {
+          std::vector<std::pair<int2, int>> v(pcs);
+          std::stable_sort(v.begin(), v.end(), [](const std::pair<int2, int>& a, const std::pair<int2, int>& b) {
+            return a.second > b.second;
+          });
+          std::vector<int> load(nsimd, 0), fill(nsimd, 0);
+          std::vector<int2> d((size_t)per_group, int2{-1, -1});
+          for (auto& pc : v) {
+            int b = -1;
+            for (int m = 0; m < nsimd; ++m)
+              if (fill[m] < wps * K2S && (b < 0 || load[m] < load[b])) b = m;
+            if (b < 0) return 1 << 30;
+            const int slot = fill[b]++;  // SIMD b's slots: wave b + nsimd * (slot % wps), super slot slot / wps
+            d[(size_t)(b + nsimd * (slot % wps)) * K2S + slot / wps] = pc.first;
+            load[b] += pc.second;
+          }
+          if (out) out->swap(d);
+          return *std::max_element(load.begin(), load.end());
+        };
+        std::vector<int> sload(nsimd, 0);
+        for (int w = 0; w < K2W; ++w) sload[w % nsimd] += wload[w];
+        int cur = *std::max_element(sload.begin(), sload.end());
+        std::vector<std::pair<int2, int>> pcs;
+        for (int2 t : order) pcs.push_back({t, ntiles(t)});
+        for (size_t x = 0; x < pcs.size() && (int)pcs.size() < per_group; ++x) {
+          const int2 t = pcs[x].first;
+          if (pcs[x].second != 4 || (t.y >> 8) != 0) continue;  // whole off-diagonal super-tiles only
+          std::vector<std::pair<int2, int>> trial(pcs);
+          trial[x] = {int2{t.x, t.y | (0xC << 8)}, 2};             // keep tiles 0, 1 (row 2 I0)
+          trial.push_back({int2{t.x, t.y | (0x3 << 8)}, 2});       // keep tiles 2, 3 (row 2 I0 + 1)
+          std::vector<int2> d;
+          const int m = simd_max(trial, &d);
+          if (m < cur) {
+            cur = m;
+            pcs.swap(trial);
+            dealt.swap(d);
+          }
+        }
+      }
+      sl.swap(dealt);
+    }
+    std::vector<int2> tl(sl.size() * 4, int2{-1, -1});
+    for (size_t k = 0; k < sl.size(); ++k) {
+      if (sl[k].x < 0) continue;
+      const int skip = sl[k].y >> 8, sy = sl[k].y & 0xFF;
       for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) {
-          const int I0 = 2 * t.x + a, J0 = 2 * t.y + b;
-          n += (I0 <= J0 && J0 < e->ntc) ? 1 : 0;
+          const int I0 = 2 * sl[k].x + a, J0 = 2 * sy + b;
+          if (I0 <= J0 && I0 < e->ntc && J0 < e->ntc && !((skip >> (2 * a + b)) & 1)) tl[4 * k + 2 * a + b] = int2{I0, J0};
         }
-      return n;
-    };
-    std::vector<int2> order(sl);
-    std::stable_sort(order.begin(), order.end(), [&](int2 a, int2 b) { return ntiles(a) > ntiles(b); });
-    const int nsimd = 4, wps = K2W / nsimd;  // waves per SIMD
-    std::vector<int2> dealt((size_t)e->ngroups * per_group, int2{-1, -1});
-    std::vector<int> gload(e->ngroups, 0), wload((size_t)e->ngroups * K2W, 0),
-        wfill((size_t)e->ngroups * K2W, 0);
-    for (int2 t : order) {
-      const int n = ntiles(t);
-      int g = -1;
-      for (int x = 0; x < e->ngroups; ++x) {
-        int free = 0;
-        for (int w = 0; w < K2W; ++w) free += K2S - wfill[x * K2W + w];
-        if (free > 0 && (g < 0 || gload[x] < gload[g])) g = x;
-      }
-      int bw = -1;
-      for (int w = 0; w < K2W; ++w) {
-        if (wfill[g * K2W + w] >= K2S) continue;
-        const int sm = w % nsimd;
-        int sl_load = 0;
-        for (int k = 0; k < wps; ++k) sl_load += wload[g * K2W + sm + nsimd * k];
-        int bl = 0;
-        if (bw >= 0)
-          for (int k = 0; k < wps; ++k) bl += wload[g * K2W + bw % nsimd + nsimd * k];
-        if (bw < 0 || sl_load < bl || (sl_load == bl && wload[g * K2W + w] < wload[g * K2W + bw])) bw = w;
-      }
-      dealt[(size_t)(g * K2W + bw) * K2S + wfill[g * K2W + bw]] = t;
-      ++wfill[g * K2W + bw];
-      wload[g * K2W + bw] += n;
-      gload[g] += n;
     }
-    if (e->ngroups == 1) {
-      // One workgroup holds every super-tile: split off-diagonal super-tiles into row halves (two tiles each,
-      // sharing their A fragment; the skipped half rides in sp.y >> 8, k2_tile_skip) while free slots remain
-      // and the busiest SIMD gets lighter.  Spot: 15 super-tiles of 3-4 tiles, busiest SIMD 15 -> 14 tiles.
-      auto simd_max = [&](const std::vector<std::pair<int2, int>>& pcs, std::vector<int2>* out) {
-        std::vector<std::pair<int2, int>> v(pcs);
-        std::stable_sort(v.begin(), v.end(), [](const std::pair<int2, int>& a, const std::pair<int2, int>& b) {
-          return a.second > b.second;
-        });
-        std::vector<int> load(nsimd, 0), fill(nsimd, 0);
-        std::vector<int2> d((size_t)per_group, int2{-1, -1});
-        for (auto& pc : v) {
-          int b = -1;
-          for (int m = 0; m < nsimd; ++m)
-            if (fill[m] < wps * K2S && (b < 0 || load[m] < load[b])) b = m;
-          if (b < 0) return 1 << 30;
-          const int slot = fill[b]++;  // SIMD b's slots: wave b + nsimd * (slot % wps), super slot slot / wps
-          d[(size_t)(b + nsimd * (slot % wps)) * K2S + slot / wps] = pc.first;
-          load[b] += pc.second;
-        }
-        if (out) out->swap(d);
-        return *std::max_element(load.begin(), load.end());
-      };
-      std::vector<int> sload(nsimd, 0);
-      for (int w = 0; w < K2W; ++w) sload[w % nsimd] += wload[w];
-      int cur = *std::max_element(sload.begin(), sload.end());
-      std::vector<std::pair<int2, int>> pcs;
-      for (int2 t : order) pcs.push_back({t, ntiles(t)});
-      for (size_t x = 0; x < pcs.size() && (int)pcs.size() < per_group; ++x) {
-        const int2 t = pcs[x].first;
-        if (pcs[x].second != 4 || (t.y >> 8) != 0) continue;  // whole off-diagonal super-tiles only
-        std::vector<std::pair<int2, int>> trial(pcs);
-        trial[x] = {int2{t.x, t.y | (0xC << 8)}, 2};             // keep tiles 0, 1 (row 2 I0)
-        trial.push_back({int2{t.x, t.y | (0x3 << 8)}, 2});       // keep tiles 2, 3 (row 2 I0 + 1)
-        std::vector<int2> d;
-        const int m = simd_max(trial, &d);
-        if (m < cur) {
-          cur = m;
-          pcs.swap(trial);
-          dealt.swap(d);
-        }
-      }
-    }
-    sl.swap(dealt);
-  }
-  std::vector<int2> tl(sl.size() * 4, int2{-1, -1});
-  for (size_t k = 0; k < sl.size(); ++k) {
-    if (sl[k].x < 0) continue;
-    const int skip = sl[k].y >> 8, sy = sl[k].y & 0xFF;
-    for (int a = 0; a < 2; ++a)
-      for (int b = 0; b < 2; ++b) {
-        const int I0 = 2 * sl[k].x + a, J0 = 2 * sy + b;
-        if (I0 <= J0 && I0 < e->ntc && J0 < e->ntc && !((skip >> (2 * a + b)) & 1)) tl[4 * k + 2 * a + b] = int2{I0, J0};
-      }
-  }
-  e->nslots = (int)tl.size();
-  std::vector<int2> both(sl);
-  both.insert(both.end(), tl.begin(), tl.end());  // d_tiles = [super slots | tile slots]
-  e->nsuper = (int)sl.size();
+    nslots = (int)tl.size();
+    std::vector<int2> both(sl);
+    both.insert(both.end(), tl.begin(), tl.end());  // d_tiles = [super slots | tile slots]
+    nsuper = (int)sl.size();
+    return both;
+  };
+  // the f64 / f32 kernels' workgroup shape for this width, and the bf16 kernel's (more slots per wave)
+  const std::vector<int2> both = deal(k2_waves(e->ntc), k2_spw(e->ntc), e->ngroups, e->nsuper, e->nslots);
+  const std::vector<int2> both_b = deal(K2_BF16_WAVES, k2_bf16_spw(e->ntc), e->ngroups_b, e->nsuper_b, e->nslots_b);
 
   hipError_t st = hipSetDevice(device);
   hipDeviceProp_t prop;
@@ -692,6 +703,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   if (st == hipSuccess) st = hipMalloc(&e->d_tiles, both.size() * sizeof(int2));
   if (st == hipSuccess) st = hipMemcpy(e->d_tiles, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMalloc(&e->d_tiles_b, both_b.size() * sizeof(int2));
+  if (st == hipSuccess) st = hipMemcpy(e->d_tiles_b, both_b.data(), both_b.size() * sizeof(int2), hipMemcpyHostToDevice);
   // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget
   if (st == hipSuccess) {
     int best = -1;
@@ -726,7 +739,7 @@ void sysid_destroy(sysid_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->d_tiles, (void*)e->d_in, (void*)e->d_panel,
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->d_tiles, (void*)e->d_tiles_b, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);

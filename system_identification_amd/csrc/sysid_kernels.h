@@ -1423,7 +1423,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // wide ones 8 waves of two slots (the LDS-DMA kernel deals its chunk rows to 8 waves).
 __host__ __device__ constexpr int k2_waves(int ntc) { return ntc < 16 ? 16 : 8; }
 __host__ __device__ constexpr int k2_spw(int ntc) { return ntc < 16 ? 1 : 2; }
-constexpr int K2_BF16_WAVES = 8;  // the bf16 kernel's waves (it takes k2_waves * k2_spw / 8 slots per wave)
+constexpr int K2_BF16_WAVES = 8;  // the bf16 kernel's waves
+// Super-tile slots per wave of the bf16 kernel.  A bf16 k-step is only 16 MFMA cycles per tile, so the kernel
+// is fed, not MFMA, bound: every super-tile group re-reads (and re-stages) the whole panel, and with the f64
+// kernels' 16 slots per group G1 (78 super-tiles) took 5 groups = 5 panel reads (G1 125k K2 3.1 ms, ~5 TB/s of
+// staged rows, the same with XCD-local groups).  Wide Grams take 5 slots per wave here (40 per group: G1 in
+// 2 groups; 80 f32 accumulator VGPRs, fragments loaded per slot); the bf16 kernel has its own super-tile deal.
+#ifndef SYSID_K2_BF16_SPW
+#define SYSID_K2_BF16_SPW 5
+#endif
+__host__ __device__ constexpr int k2_bf16_spw(int ntc) {
+  return ntc >= 16 ? SYSID_K2_BF16_SPW : k2_waves(ntc) * k2_spw(ntc) / K2_BF16_WAVES;
+}
 #ifndef SYSID_K2_UNIFORM
 #define SYSID_K2_UNIFORM 0  // readfirstlane'd descriptors measured slower (G1 K2 1.80 -> 2.26 ms, Spot +3%)
 #endif
@@ -1441,6 +1452,27 @@ template <> struct K2Acc<float> { typedef flt4 type; };
 // Super-tile slot descriptor {I0, J0 | skip << 8}: skip bit t drops tile t = 2a + b (a super-tile split into
 // row halves over two slots by the host's balancing; 0 otherwise).
 __device__ __forceinline__ bool k2_tile_skip(int2 sp, int t) { return sp.x >= 0 && ((sp.y >> (8 + t)) & 1); }
+
+// Workgroup -> (split-K slice ks, super-tile group).  Every group of a slice reads the same panel rows, so
+// with several groups (wide Grams: G1 has 5) the rows are re-read once per group.  Blocks are dealt
+// round-robin over the 8 XCDs (b and b + 8 share one, MI355X_MICROARCH.md §Workgroup dispatch), so the
+// plain ks = b / ngroups put a slice's groups on different XCDs and every re-read went to HBM / MALL
+// (G1 K2 at ~6 TB/s of re-reads).  Here the blocks of one XCD take consecutive (ks, group) pairs, so a
+// slice's groups share an L2 and run side by side: one HBM read, the others L2 hits.  A bijection for any
+// grid; speed only (any placement is correct).
+#ifndef SYSID_K2_XCD_MAP
+#define SYSID_K2_XCD_MAP 1
+#endif
+__device__ __forceinline__ void k2_block_coords(int ngroups, int& group, int& ks) {
+  int L = (int)blockIdx.x;
+  if (SYSID_K2_XCD_MAP && ngroups > 1) {
+    const int nb = (int)gridDim.x, x = L & 7, i = L >> 3;
+    const int q = nb >> 3, r = nb & 7;  // XCD y holds q + (y < r) blocks
+    L = x * q + (x < r ? x : r) + i;
+  }
+  group = L % ngroups;
+  ks = L / ngroups;
+}
 
 __host__ __device__ constexpr int k2_stride(int ntc) { return ((ntc * 16 + 31) / 32) * 32 + 16; }
 
@@ -1464,8 +1496,8 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   constexpr int BUF = KC * STRIDE;                       // elements per LDS buffer
   constexpr int NT = 64 * K2W;
   __shared__ T lds[2 * BUF];
-  const int group = blockIdx.x % ngroups;
-  const int ks = blockIdx.x / ngroups;
+  int group, ks;
+  k2_block_coords(ngroups, group, ks);
   // whole chunks per workgroup: only the panel's last chunk may be partial
   const int64_t nck = (rows + KC - 1) / KC;
   const int64_t r0 = (nck * ks / ksplit) * KC;
@@ -1694,8 +1726,8 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   constexpr int EB = (int)sizeof(T);
   static_assert(3 * BUF * EB <= 160 * 1024, "three LDS buffers");
   __shared__ __attribute__((aligned(16))) T lds[3 * BUF];
-  const int group = blockIdx.x % ngroups;
-  const int ks = blockIdx.x / ngroups;
+  int group, ks;
+  k2_block_coords(ngroups, group, ks);
   const int64_t q4 = rows / 4;
   const int64_t r0 = 4 * (q4 * ks / ksplit);
   const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
@@ -1868,15 +1900,15 @@ __global__ void __launch_bounds__(64 * K2_BF16_WAVES)
 k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
                   int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   static_assert(KC % 32 == 0, "bf16 K2 chunks are whole 32-row k-steps");
-  // always 8 waves (16 spill its transposes at 128 VGPRs), over the same slots per group as the f64 kernels
-  constexpr int K2W = K2_BF16_WAVES, K2S = k2_waves(NTC) * k2_spw(NTC) / K2_BF16_WAVES;
+  // always 8 waves (16 spill its transposes at 128 VGPRs), k2_bf16_spw(NTC) super-tile slots each
+  constexpr int K2W = K2_BF16_WAVES, K2S = k2_bf16_spw(NTC);
   constexpr int NCOL = NTC * 16;
   constexpr int CS = KC + 8;
   constexpr int BUF = NCOL * CS;
   constexpr int NT = 64 * K2W;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
-  const int group = blockIdx.x % ngroups;
-  const int ks = blockIdx.x / ngroups;
+  int group, ks;
+  k2_block_coords(ngroups, group, ks);
   const int64_t q4 = rows / 4;
   const int64_t r0 = 4 * (q4 * ks / ksplit);
   const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
@@ -1962,17 +1994,17 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
     if (c + 1 < nchunks) load_chunk(r0 + (c + 1) * KC);
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 32) {
-      bf16x8 x[4 * K2S];
-#pragma unroll
-      for (int u = 0; u < 4 * K2S; ++u) x[u] = *reinterpret_cast<const bf16x8*>(cur + foff[u] + kk);
 #pragma unroll
       for (int s = 0; s < K2S; ++s) {
+        // one slot's four fragments at a time (all of them at once would hold 4 K2S x 4 VGPRs)
+        bf16x8 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const bf16x8*>(cur + foff[4 * s + u] + kk);
         constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           if (need[s][t])
-            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t],
-                                                               0, 0, 0);
+            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[AB[t][0]], x[AB[t][1]], acc[s][t], 0, 0, 0);
       }
     }
     if (c + 1 < nchunks) store_chunk(lds + ((c + 1) & 1) * BUF);
