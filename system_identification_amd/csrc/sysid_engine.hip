@@ -51,10 +51,12 @@ struct sysid_engine {
   int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4, k1_variant = 0;
   size_t k1_lds = 0;
   // K2/K3 Gram tiling
-  int ntc = 0, nslots = 0, nsuper = 0, ngroups = 0;
-  int2* d_tiles = nullptr;
-  int nslots_b = 0, nsuper_b = 0, ngroups_b = 0;  // the bf16 kernel's deal (k2_bf16_spw slots per wave)
-  int2* d_tiles_b = nullptr;
+  int ntc = 0;
+  // super-tile deal per Gram arithmetic (0 f64, 1 f32, 2 bf16): each kernel's waves x slots per wave
+  struct Deal {
+    int ngroups = 0, nsuper = 0, nslots = 0;
+    int2* d_tiles = nullptr;  // [super slots | tile slots]
+  } k2d[3];
   // host-API buffers (grow-only)
   double* d_in = nullptr;
   size_t in_cap = 0;
@@ -98,14 +100,13 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
   // the bf16 kernel's large chunks take most of a CU's LDS: one workgroup per CU
   const int mult = (e->ntc >= 16 || (SYSID_K2_DMA_NARROW && e->ntc <= 10)) && prec != 2 ? 2 : 1;
-  int ks = std::max(1, mult * e->cus / std::max(1, prec == 2 ? e->ngroups_b : e->ngroups));
+  int ks = std::max(1, mult * e->cus / std::max(1, e->k2d[prec].ngroups));
   const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
 }
 
 size_t slab_bytes(const sysid_engine* e, int64_t rows, int prec = 0) {
-  const int nslots = prec == 2 ? e->nslots_b : e->nslots;
-  return align256((size_t)ksplit_for(e, rows, prec) * nslots * 256 * sizeof(double));
+  return align256((size_t)ksplit_for(e, rows, prec) * e->k2d[prec].nslots * 256 * sizeof(double));
 }
 
 int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
@@ -214,7 +215,8 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
               double* slab, hipStream_t st, int prec) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
-  const dim3 g2(e->ngroups * ks), b2(64 * k2_waves(e->ntc));
+  const sysid_engine::Deal& D = e->k2d[prec];
+  const dim3 g2(D.ngroups * ks), b2(64 * k2_waves(e->ntc));
   const double* p64 = static_cast<const double*>(d_panel);
   const float* p32 = static_cast<const float*>(d_panel);
   const __bf16* p16 = static_cast<const __bf16*>(d_panel);
@@ -224,17 +226,17 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
 #define SYSID_K2_F64(NTC, KC)                                                                                \
   if constexpr (SYSID_K2_DMA && (NTC >= 16 || (SYSID_K2_DMA_NARROW && NTC <= 10)))                           \
     hipLaunchKernelGGL((k2_gram_syrk_dma<double, NTC, k2_dma_kc(NTC)>), g2, b2, 0, st, p64, rows, ld_panel,    \
-                       e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                            \
+                       D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);                            \
   else                                                                                                      \
-    hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, e->d_tiles,       \
-                       e->ngroups, ks, e->nslots, accumulate, slab);
+    hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, D.d_tiles,       \
+                       D.ngroups, ks, D.nslots, accumulate, slab);
 #define SYSID_K2_F32(NTC, KC) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                   \
   if constexpr (SYSID_K2_DMA && (NTC >= 16 || (SYSID_K2_DMA_NARROW && NTC <= 10)))                           \
     hipLaunchKernelGGL((k2_gram_syrk_dma<float, NTC, 2 * k2_dma_kc(NTC)>), g2, b2, 0, st, p32, rows, ld_panel, \
-                       e->d_tiles, e->ngroups, ks, e->nslots, accumulate, slab);                            \
+                       D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);                            \
   else                                                                                                      \
-    hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, e->d_tiles,    \
-                       e->ngroups, ks, e->nslots, accumulate, slab);
+    hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, D.d_tiles,    \
+                       D.ngroups, ks, D.nslots, accumulate, slab);
 #define SYSID_K2_CASE(NTC, KC)                                                                               \
   case NTC:                                                                                                 \
     if (prec == 0) {                                                                                        \
@@ -242,9 +244,8 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
     } else if (prec == 1) {                                                                                 \
       SYSID_K2_F32(NTC, KC)                                                                                 \
     } else {                                                                                                \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), dim3(e->ngroups_b * ks),                  \
-                         dim3(64 * K2_BF16_WAVES), 0, st, p16, rows, ld_panel,                              \
-                         e->d_tiles_b, e->ngroups_b, ks, e->nslots_b, accumulate, slab);                    \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16,   \
+                         rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);             \
     }                                                                                                       \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
@@ -262,9 +263,9 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
 }
 
 int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st, int prec = 0) {
-  const bool b = prec == 2;  // the bf16 kernel's slabs follow its own deal
-  const int64_t nx = (int64_t)(b ? e->nslots_b : e->nslots) * 256;
-  const int2* tiles = b ? e->d_tiles_b + e->nsuper_b : e->d_tiles + e->nsuper;
+  const sysid_engine::Deal& D = e->k2d[prec];  // the slabs follow the K2 kernel's own deal
+  const int64_t nx = (int64_t)D.nslots * 256;
+  const int2* tiles = D.d_tiles + D.nsuper;
   hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, tiles, nx, ks, e->ncol,
                      d_gram);
   HIP_TRY(e, hipGetLastError());
@@ -688,8 +689,13 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     return both;
   };
   // the f64 / f32 kernels' workgroup shape for this width, and the bf16 kernel's (more slots per wave)
-  const std::vector<int2> both = deal(k2_waves(e->ntc), k2_spw(e->ntc), e->ngroups, e->nsuper, e->nslots);
-  const std::vector<int2> both_b = deal(K2_BF16_WAVES, k2_bf16_spw(e->ntc), e->ngroups_b, e->nsuper_b, e->nslots_b);
+  std::vector<int2> dealt[3];
+  for (int p = 0; p < 3; ++p) {
+    sysid_engine::Deal& D = e->k2d[p];
+    const int w = p == 2 ? K2_BF16_WAVES : k2_waves(e->ntc);
+    const int sp = p == 0 ? k2_slots<double>(e->ntc) : p == 1 ? k2_slots<float>(e->ntc) : k2_bf16_spw(e->ntc);
+    dealt[p] = deal(w, sp, D.ngroups, D.nsuper, D.nslots);
+  }
 
   hipError_t st = hipSetDevice(device);
   hipDeviceProp_t prop;
@@ -701,10 +707,11 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
   if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
-  if (st == hipSuccess) st = hipMalloc(&e->d_tiles, both.size() * sizeof(int2));
-  if (st == hipSuccess) st = hipMemcpy(e->d_tiles, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice);
-  if (st == hipSuccess) st = hipMalloc(&e->d_tiles_b, both_b.size() * sizeof(int2));
-  if (st == hipSuccess) st = hipMemcpy(e->d_tiles_b, both_b.data(), both_b.size() * sizeof(int2), hipMemcpyHostToDevice);
+  for (int p = 0; p < 3; ++p) {
+    int2*& t = e->k2d[p].d_tiles;
+    if (st == hipSuccess) st = hipMalloc(&t, dealt[p].size() * sizeof(int2));
+    if (st == hipSuccess) st = hipMemcpy(t, dealt[p].data(), dealt[p].size() * sizeof(int2), hipMemcpyHostToDevice);
+  }
   // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget
   if (st == hipSuccess) {
     int best = -1;
@@ -739,7 +746,7 @@ void sysid_destroy(sysid_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->d_tiles, (void*)e->d_tiles_b, (void*)e->d_in, (void*)e->d_panel,
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);

@@ -1429,6 +1429,15 @@ constexpr int K2_BF16_WAVES = 8;  // the bf16 kernel's waves
 // kernels' 16 slots per group G1 (78 super-tiles) took 5 groups = 5 panel reads (G1 125k K2 3.1 ms, ~5 TB/s of
 // staged rows, the same with XCD-local groups).  Wide Grams take 5 slots per wave here (40 per group: G1 in
 // 2 groups; 80 f32 accumulator VGPRs, fragments loaded per slot); the bf16 kernel has its own super-tile deal.
+// Super-tile slots per wave of the f64 / f32 kernels.  Wide f32 Grams take more (f32 accumulators are half
+// the f64 registers), so fewer groups re-read the panel (see k2_bf16_spw below).
+#ifndef SYSID_K2_F32_SPW
+#define SYSID_K2_F32_SPW 2
+#endif
+template <typename T>
+__host__ __device__ constexpr int k2_slots(int ntc) {
+  return sizeof(T) == 4 && ntc >= 16 ? SYSID_K2_F32_SPW : k2_spw(ntc);
+}
 #ifndef SYSID_K2_BF16_SPW
 #define SYSID_K2_BF16_SPW 5
 #endif
@@ -1491,7 +1500,7 @@ __global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
              int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   typedef typename K2Acc<T>::type accT;
-  constexpr int K2W = k2_waves(NTC), K2S = k2_spw(NTC);
+  constexpr int K2W = k2_waves(NTC), K2S = k2_slots<T>(NTC);
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;                       // elements per LDS buffer
   constexpr int NT = 64 * K2W;
@@ -1717,7 +1726,7 @@ __global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
                  int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   typedef typename K2Acc<T>::type accT;
-  constexpr int K2W = k2_waves(NTC), K2S = k2_spw(NTC);
+  constexpr int K2W = k2_waves(NTC), K2S = k2_slots<T>(NTC);
   static_assert(KC % K2W == 0 && KC % 4 == 0, "chunk rows are dealt to the waves, k-steps of 4");
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;  // elements per LDS buffer
