@@ -133,13 +133,17 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
 #ifndef SYSID_K1_QCH
 #define SYSID_K1_QCH 3
 #endif
-enum { K1_C4_NV18, K1_C4, K1_C16 };
+enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16 };
+#ifndef SYSID_K1_C12
+#define SYSID_K1_C12 1  // a 12-slot instantiation for chains of 5..12 revolute joints (G1: 10)
+#endif
+int k1_chain_slots(int maxch) { return maxch <= 4 ? 4 : (SYSID_K1_C12 && maxch <= 12) ? 12 : 16; }
 
 // maxch: the longest revolute chain.  The nv = 18 kernel unrolls SYSID_K1_QCH chain slots.
 int k1_variant(int maxch, int nv, int nbody) {
   // the nv = 18 kernel stages two panel rows of all bodies (lane = body x row group: 11..16 bodies)
   if (maxch <= SYSID_K1_QCH && nv == 18 && nbody >= 11 && nbody <= 16) return K1_C4_NV18;
-  return maxch <= 4 ? K1_C4 : K1_C16;
+  return maxch <= 4 ? K1_C4 : k1_chain_slots(maxch) == 12 ? K1_C12 : K1_C16;
 }
 
 int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : SYSID_K1_SPW_GEN; }
@@ -151,6 +155,7 @@ const void* k1_fn(int variant) {
   switch (variant) {
     case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, double>);
     case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, double>);
+    case K1_C12: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, double>);
     default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, double>);
   }
 }
@@ -173,6 +178,10 @@ void k1_launch_typed(sysid_engine* e, dim3 g1, dim3 b1, hipStream_t st, const K1
     case K1_C4:
       hipLaunchKernelGGL((k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in,
                          N, ld, d_panel, ld_panel, work, dbg);
+      break;
+    case K1_C12:
+      hipLaunchKernelGGL((k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
+                         d_in, N, ld, d_panel, ld_panel, work, dbg);
       break;
     default:
       hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
@@ -529,7 +538,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (in_lds > IN_MAX) return set_err(nullptr, SYSID_E_MODEL, "too many input channels (%d > %d)", in_lds, IN_MAX);
 
   // model image (layout sysid_dev::mimg_layout)
-  const int maxch_tpl = maxch <= 4 ? 4 : 16;
+  const int maxch_tpl = k1_chain_slots(maxch);
   const MImg MI = mimg_layout(NJ, nv, nc, maxch_tpl);
   std::vector<uint32_t> img((size_t)MI.ndbl * 2, 0u);
   int* ii = reinterpret_cast<int*>(img.data());
