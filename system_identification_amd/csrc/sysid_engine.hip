@@ -133,7 +133,9 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
 #ifndef SYSID_K1_QCH
 #define SYSID_K1_QCH 3
 #endif
-enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16 };
+enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16, K1_C12P, K1_C16P };  // ...P: the P-overlay layout (wave_layout pov)
+int k1_pov_variant(int variant) { return variant == K1_C12 ? K1_C12P : variant == K1_C16 ? K1_C16P : -1; }
+bool k1_is_pov(int variant) { return variant == K1_C12P || variant == K1_C16P; }
 #ifndef SYSID_K1_C12
 #define SYSID_K1_C12 1  // a 12-slot instantiation for chains of 5..12 revolute joints (G1: 10)
 #endif
@@ -156,6 +158,8 @@ const void* k1_fn(int variant) {
     case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, double>);
     case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, double>);
     case K1_C12: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, double>);
+    case K1_C12P: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, double, 1>);
+    case K1_C16P: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, double, 1>);
     default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, double>);
   }
 }
@@ -181,6 +185,14 @@ void k1_launch_typed(sysid_engine* e, dim3 g1, dim3 b1, hipStream_t st, const K1
       break;
     case K1_C12:
       hipLaunchKernelGGL((k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
+                         d_in, N, ld, d_panel, ld_panel, work, dbg);
+      break;
+    case K1_C12P:
+      hipLaunchKernelGGL((k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
+                         d_in, N, ld, d_panel, ld_panel, work, dbg);
+      break;
+    case K1_C16P:
+      hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
                          d_in, N, ld, d_panel, ld_panel, work, dbg);
       break;
     default:
@@ -571,7 +583,21 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->in_rows = in_rows;
   e->in_lds = in_lds;
   e->k1_variant = k1_variant(maxch, nv, NJ - 1);
-  const WLay WL = wave_layout(in_lds, nv, NJ, nc, k1_layout_hw(e->k1_variant));
+  const int lhw = k1_layout_hw(e->k1_variant);
+  const WLay WL0 = wave_layout(in_lds, nv, NJ, nc, lhw);
+  // P overlay (wave_layout `pov`): runtime-nv kernels whose H1 is read from P (an even free-flyer offset), when
+  // D's working set fits under P's slot and the passes landing on it fit the kernel's register buffer
+  bool pov_ok = false;
+  WLay WL1 = WL0;
+  if (lhw == 0 && k1_pov_variant(e->k1_variant) >= 0 && nff > 0 && (ff0 & 1) == 0) {
+    const int pp = (nv * nv + 1) & ~1, qsize = WL0.P - WL0.Jc;
+    if (qsize <= pp) {
+      WL1 = wave_layout(in_lds, nv, NJ, nc, lhw, 1);
+      const int passes = (nv * nv + 63) / 64, t0 = (WL1.Jc - WL1.P) / 64;
+      pov_ok = passes - t0 <= K1_POV_BUF;
+    }
+  }
+  WLay WL = WL0;
   K1Params& kp = e->kp;
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
@@ -724,14 +750,33 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget
   if (st == hipSuccess) {
     int best = -1;
-    for (int wv : {4, 2, 1}) {
-      const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(e->k1_variant) * WL.total) * sizeof(double);
-      if (lds > 160 * 1024) continue;
-      (void)hipFuncSetAttribute(k1_fn(e->k1_variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k1_fn(e->k1_variant), 64 * wv, lds) != hipSuccess) nb = 0;
-      if (nb * wv > best) { best = nb * wv; e->k1_waves = wv; e->k1_blocks_per_cu = std::max(1, nb); e->k1_lds = lds; }
+    // layouts: the plain one first (kept on ties), then the P overlay; 8-wave workgroups for one-sample waves
+#ifndef SYSID_K1_POV
+#define SYSID_K1_POV 1
+#endif
+    const int v0 = e->k1_variant;
+    for (int ov = 0; ov < (SYSID_K1_POV && pov_ok ? 2 : 1); ++ov) {
+      const WLay& wl = ov ? WL1 : WL0;
+      const int var = ov ? k1_pov_variant(v0) : v0;
+      for (int wv : {8, 4, 2, 1}) {
+        if (wv > K1_WAVES && !k1_is_pov(var)) continue;  // 8-wave workgroups: the overlay instantiations only
+        const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(var) * wl.total) * sizeof(double);
+        if (lds > 160 * 1024) continue;
+        (void)hipFuncSetAttribute(k1_fn(var), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k1_fn(var), 64 * wv, lds) != hipSuccess) nb = 0;
+        if (nb * wv > best) {
+          best = nb * wv;
+          e->k1_waves = wv;
+          e->k1_blocks_per_cu = std::max(1, nb);
+          e->k1_lds = lds;
+          e->k1_variant = var;
+          WL = wl;
+          kp.pov = ov;
+        }
+      }
     }
+    kp.wave_dbl = WL.total;
     if (best <= 0) {
       set_err(nullptr, SYSID_E_MODEL, "model needs too much LDS per sample (%zu B)", (size_t)WL.total * 8);
       sysid_destroy(e);
@@ -1131,7 +1176,7 @@ int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6) {
 
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
   if (!e || !offsets12) return SYSID_E_INVALID;
-  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant));
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant), e->kp.pov);
   const int o[12] = {L.in, L.body, L.W, L.Pt, L.Jw, L.pf, L.Jc, L.M, L.P, L.H1, L.tp, L.total};
   for (int k = 0; k < 12; ++k) offsets12[k] = o[k];
   return SYSID_OK;
@@ -1140,7 +1185,7 @@ int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
 int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
                         const double* cnt, double* lds_image, int64_t image_doubles) {
   if (!e || !lds_image) return set_err(e, SYSID_E_INVALID, "null argument");
-  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant));
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant), e->kp.pov);
   if (image_doubles < L.total) return set_err(e, SYSID_E_INVALID, "image needs %d doubles", L.total);
   HIP_TRY(e, hipSetDevice(e->device));
   int rc = sysid_build(e, q, dq, ddq, tau, cnt, 1, 1, SYSID_EMIT_Y, nullptr, nullptr, nullptr, nullptr, nullptr,

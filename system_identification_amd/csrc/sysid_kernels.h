@@ -77,12 +77,16 @@ constexpr int BODY_STRIDE = 26;
 //     a pass may overwrite the Z rows the passes before it consumed; P starts `margin` doubles before Z,
 //     the largest lead of the written entries over the consumed Z rows (over M, dead after Z is built).
 //     Spot: 1,582 -> 1,158 doubles per sample, so 8 two-sample waves share a CU's 160 KB (was 6).
-//   * otherwise P follows D.
+//   * otherwise P follows D, or, with `pov` (P overlay, runtime-nv kernels whose H1 is read from P), P starts
+//     at D and D's working set moves to the tail of P's slot: the P pass buffers the entries that land on it
+//     in registers until every entry has been computed (K1_POV_BUF passes at most).  G1: 2,916 -> 2,452
+//     doubles per sample, so one workgroup of 8 one-sample waves fits a CU's 160 KB (was 3 x 2 waves).
+constexpr int K1_POV_BUF = 12;  // P passes (of 64 entries) a P overlay may hold in registers
 struct WLay {
   int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, dqs, Z, total;
 };
 
-__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc, int hw) {
+__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc, int hw, int pov = 0) {
   WLay l;
   const int k = 3 * nc;
   int o = 0;
@@ -114,6 +118,14 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc,
   if (hw > 0) {
     l.P = u0 - r2(margin);      // P = I - Q^T Q
     grow(l.P + r2(nv * nv));
+  } else if (pov) {
+    // D's working set [Jc .. end) moves to the tail of P's slot [D, D + r2(nv nv)) (the caller checked it fits)
+    const int shift = r2(nv * nv) - (o - D);
+    l.Jc += shift; l.M += shift; l.W += shift; l.Pt += shift; l.pf += shift; l.Z += shift;
+    l.P = D;
+    l.H1 = D;  // unused: H1 is read from P's free-flyer columns
+    l.total = D + r2(nv * nv);
+    return l;
   } else {
     l.P = take(nv * nv);
   }
@@ -128,6 +140,7 @@ struct K1Params {
   int in_lds;       // input channels the LDS layout holds (in_rows of the full-force mode)
   int full;         // 1: get_full_regressor_force mode (P = I, tau column = S^T tau + J_c^T lambda)
   int rg;           // row groups of the regressor-column phase (lanes = bodies x rg)
+  int pov;          // 1: P overlays the projector's working set (wave_layout `pov`)
   double thr_rel;   // rank cut of the projector: remaining row norm <= thr_rel * the largest row norm
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
 };
@@ -442,7 +455,7 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 #ifndef SYSID_EXP_SKIP
 #define SYSID_EXP_SKIP 0  // diagnostics builds only: bit mask of K1 phases to skip (timing attribution)
 #endif
-template <int MAXCH, int NVC, int SPW, typename OutT>
+template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0>
 #ifndef SYSID_K1_MIN_WAVES_PER_EU
 #define SYSID_K1_MIN_WAVES_PER_EU 1
 #endif
@@ -450,7 +463,8 @@ template <int MAXCH, int NVC, int SPW, typename OutT>
 #define SYSID_PRIO 1  // column phase at low issue priority, the latency-bound phases high (K1 -2%)
 #endif
 // Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
-__global__ void __launch_bounds__(64 * K1_WAVES, SPW == 2 ? 2 : SYSID_K1_MIN_WAVES_PER_EU)
+// The P overlay's instantiations run 8 one-sample waves per workgroup (one 8-wave workgroup per CU).
+__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 ? 2 : SYSID_K1_MIN_WAVES_PER_EU)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
                    int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
                    unsigned long long* __restrict__ work, double* __restrict__ dbg) {
@@ -487,7 +501,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   constexpr bool CHAIN_UNCOND = NVC == 18;  // unconditional chain loads in the column phase
   constexpr int HW = 64 / SPW;                       // lanes per sample
   const int half = lane / HW, hl = lane % HW;         // sample slot within the wave, lane within it
-  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0);
+  static_assert(POV == 0 || NVC == 0, "the P overlay is a runtime-nv layout");
+  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0, POV);
   double* wr = smem + kp.mimg_dbl + (wave * SPW + half) * kp.wave_dbl;
   double* body = wr + L.body;
   double* Ws = wr + L.W;
@@ -820,12 +835,15 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // in place (an even ff0 keeps the rows' 16-byte alignment); otherwise H1 is copied out below.
     const bool h1_in_p = kp.has_ff && (kp.ff0 & 1) == 0;
     if (kp.full) {
-      // get_full_regressor_force (src/sys_identification.py:391-399): no projection
-      for (int e = hl; e < nv * nv; e += HW) {
-        const int a = e / nv;
-        Ps[e] = e - a * nv == a ? 1.0 : 0.0;
+      // get_full_regressor_force (src/sys_identification.py:391-399): no projection.  With the overlay P = I
+      // is written after the tau column below (which reads J_c, under P's slot there).
+      if constexpr (!POV) {
+        for (int e = hl; e < nv * nv; e += HW) {
+          const int a = e / nv;
+          Ps[e] = e - a * nv == a ? 1.0 : 0.0;
+        }
+        wsync();
       }
-      wsync();
     } else {
       // ---- orthonormal basis of J_c's row space by modified Gram-Schmidt ----
       // P = I - pinv(J_c) J_c is the projector onto null(J_c) = I - Q^T Q for any orthonormal basis Q of
@@ -1017,14 +1035,43 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         wsync();
       } else {
         // Runtime-nv kernels: P has its own region (wave_layout with hw = 0), so its passes need no
-        // ordering point between them.
-        for (int e = hl; e < nv * nv; e += HW) {
-          const int a = e / nv, b = e - a * nv;
-          const double* za = Zt + a * K;
-          double acc = 0.0;
+        // ordering point between them; with the overlay (POV) the passes whose entries land on J_c / Z
+        // (the slot's tail, from entry L.Jc - L.P on) are held in registers until every entry is computed.
+        if constexpr (POV) {
+          auto p_entry = [&](int e) -> double {
+            const int a = e / nv, b = e - a * nv;
+            const double* za = Zt + a * K;
+            double acc = 0.0;
 #pragma unroll 4
-          for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
-          Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+            for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
+            return (a == b ? 1.0 : 0.0) - acc;
+          };
+          const int t0 = (L.Jc - L.P) / HW;  // first buffered pass
+          for (int t = 0; t < t0; ++t) {
+            const int e = hl + HW * t;
+            if (e < nv * nv) Ps[e] = p_entry(e);
+          }
+          double pb[K1_POV_BUF];
+#pragma unroll
+          for (int u = 0; u < K1_POV_BUF; ++u) {
+            const int e = hl + HW * (t0 + u);
+            pb[u] = e < nv * nv ? p_entry(e) : 0.0;
+          }
+          wsync();  // every entry computed: the overlaid J_c / Z are dead
+#pragma unroll
+          for (int u = 0; u < K1_POV_BUF; ++u) {
+            const int e = hl + HW * (t0 + u);
+            if (e < nv * nv) Ps[e] = pb[u];
+          }
+        } else {
+          for (int e = hl; e < nv * nv; e += HW) {
+            const int a = e / nv, b = e - a * nv;
+            const double* za = Zt + a * K;
+            double acc = 0.0;
+#pragma unroll 4
+            for (int j = 0; j < k; ++j) acc += za[j] * Jc[j * nv + b];
+            Ps[e] = (a == b ? 1.0 : 0.0) - acc;
+          }
         }
         wsync();
       }
@@ -1037,8 +1084,12 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     // tp first: in the full mode H1 may be stored over J_c (overlay layout), which the tau column reads.
     for (int r = hl; r < nv; r += HW) {
       double acc = 0.0;
+      if (POV && kp.full) {
+        acc = r >= bd && r < bd + nja ? tau[r - bd] : 0.0;  // P = I (not yet written)
+      } else {
 #pragma unroll 4
-      for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
+        for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
+      }
       if (kp.full) {
         // + J_c^T lambda, lambda = the measured forces of the feet in contact in foot order, world axes
         // (LOCAL_WORLD_ALIGNED).  J_c here is in base axes, J_c,world = R_b J_c, so lambda is moved to
@@ -1064,7 +1115,15 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       tps[r] = acc;
     }
-    if (kp.full) wsync();
+    if (kp.full && !POV) wsync();
+    if (POV && kp.full) {
+      wsync();  // J_c read: P = I may overwrite it now
+      for (int e = hl; e < nv * nv; e += HW) {
+        const int a = e / nv;
+        Ps[e] = e - a * nv == a ? 1.0 : 0.0;
+      }
+      wsync();
+    }
     for (int e = hl; e < nv * 6 && !h1_in_p; e += HW) {
       const int r = e / 6, c = e - 6 * r;
       H1[e] = kp.has_ff ? Ps[r * nv + kp.ff0 + c] : 0.0;  // J_w[:, ff] = I (see h1_in_p)
