@@ -334,6 +334,34 @@ def test_reduced_precision_gram(robot, N):
     assert np.array_equal(out["f32"], out["f32"].T) and np.array_equal(out["bf16"], out["bf16"].T)
 
 
+@pytest.mark.parametrize("robot,N", [("spot", 20000), ("g1_29dof", 5000)])
+def test_reduced_precision_gram_matches_rounded_panel(robot, N):
+    """The f32 / bf16 Gram kernels (each with its own super-tile deal and K3 reduction) against the exact
+    Gram of the panel rounded the way K1 rounds it (f64 -> f32, then -> bf16, both RNE): what remains is only
+    the kernels' f32 accumulation, so the bound is tight (1e-5 normwise), unlike the error against the f64
+    Gram that test_reduced_precision_gram reports.  Gram-only output vs the full path's f64 panel."""
+    import torch
+    model = load_robot(robot)
+    e = eng(robot)
+    d = generate(model, N, config_index=7)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_device(N, EMIT_ALL)
+    e.build_device(din, N, EMIT_ALL, bufs)
+    torch.cuda.synchronize()
+    p64 = bufs["panel"][:, :e.panel_cols]
+    rounded = {"f32": p64.to(torch.float32).to(torch.float64),
+               "bf16": p64.to(torch.float32).to(torch.bfloat16).to(torch.float64)}
+    for prec, pr in rounded.items():
+        ref = (pr.T @ pr).cpu().numpy()
+        g = e.alloc_gram_device(N)
+        e.build_gram_device(din, N, g, precision=prec)
+        torch.cuda.synchronize()
+        G = g["gram"].cpu().numpy()
+        err = np.linalg.norm(G - ref) / np.linalg.norm(ref)
+        print(f"{robot} N={N} {prec} Gram vs the Gram of the {prec}-rounded panel: {err:.2e}")
+        assert err < 1e-5, (prec, err)
+
+
 @pytest.mark.parametrize("robot,N,cfg", [("solo12", 48, 0), ("spot", 64, 1), ("g1_29dof", 24, 2),
                                          ("solo12_fixed", 48, 3)])
 def test_full_regressor_force_vs_oracle(robot, N, cfg):
