@@ -265,8 +265,12 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
     } else if (prec == 1) {                                                                                 \
       SYSID_K2_F32(NTC, KC)                                                                                 \
     } else {                                                                                                \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16,   \
-                         rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);             \
+      if constexpr (SYSID_K2_BF16_TR && NTC >= 16)                                                          \
+        hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0,  \
+                           st, p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);  \
+      else                                                                                                  \
+        hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st,  \
+                           p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);      \
     }                                                                                                       \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)

@@ -1500,8 +1500,15 @@ __host__ __device__ constexpr int k2_slots(int ntc) {
 #ifndef SYSID_K2_BF16_SPW
 #define SYSID_K2_BF16_SPW 5
 #endif
+#ifndef SYSID_K2_BF16_TR
+#define SYSID_K2_BF16_TR 1  // wide Grams on k2_gram_syrk_bf16_tr (LDS-DMA + transposed fragment reads)
+#endif
+#ifndef SYSID_K2_BF16_TR_SPW
+#define SYSID_K2_BF16_TR_SPW 10
+#endif
 __host__ __device__ constexpr int k2_bf16_spw(int ntc) {
-  return ntc >= 16 ? SYSID_K2_BF16_SPW : k2_waves(ntc) * k2_spw(ntc) / K2_BF16_WAVES;
+  return ntc >= 16 ? (SYSID_K2_BF16_TR ? SYSID_K2_BF16_TR_SPW : SYSID_K2_BF16_SPW)
+                   : k2_waves(ntc) * k2_spw(ntc) / K2_BF16_WAVES;
 }
 #ifndef SYSID_K2_UNIFORM
 #define SYSID_K2_UNIFORM 0  // readfirstlane'd descriptors measured slower (G1 K2 1.80 -> 2.26 ms, Spot +3%)
@@ -2081,6 +2088,168 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
 #pragma unroll
   for (int s = 0; s < K2S; ++s) {
     if (!live[s]) continue;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double* x = o + (4 * (lane >> 4) + j) * 16 + (lane & 15);
+        const double v = (double)acc[s][t][j];
+        *x = accumulate ? *x + v : v;
+      }
+    }
+  }
+}
+
+// K2 bf16, wide Grams: the panel is staged by LDS-DMA into three row-major buffers (no staging registers, no
+// transpose pass, two chunks in flight) and every MFMA fragment is read transposed by two ds_read_b64_tr_b16
+// (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane i receives column i
+// of the 4 rows), so one workgroup holds all super-tiles of G1 (10 slots per wave, 160 f32 accumulator VGPRs)
+// and the panel is read once.  Reads are issued by every lane (EXEC all ones: the gather crosses lanes).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 k2_frag_tr(const __bf16* p, int stride) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p + 4 * stride));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Rows per chunk of the transposed-read kernel: three row-major buffers of NTC*16 + 8 bf16 per row in 160 KB.
+__host__ __device__ constexpr int k2_bf16_tr_kc(int ntc) {
+  return (160 * 1024 / (3 * (ntc * 16 + 8) * 2)) / 32 * 32 > 128 ? 128 : (160 * 1024 / (3 * (ntc * 16 + 8) * 2)) / 32 * 32;
+}
+
+template <int NTC, int KC>
+__global__ void __launch_bounds__(64 * K2_BF16_WAVES)
+k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+                     int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+  static_assert(KC % 32 == 0 && KC % K2_BF16_WAVES == 0, "whole 32-row k-steps, rows dealt to the waves");
+  constexpr int K2W = K2_BF16_WAVES, K2S = k2_bf16_spw(NTC);
+  constexpr int STRIDE = NTC * 16 + 8;  // elements per LDS row (16-byte multiple)
+  constexpr int BUF = KC * STRIDE;
+  constexpr int NT = 64 * K2W;
+  constexpr int RPW = KC / K2W;
+  static_assert(3 * BUF * 2 <= 160 * 1024, "three LDS buffers");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
+  int group, ks;
+  k2_block_coords(ngroups, group, ks);
+  const int64_t q4 = rows / 4;
+  const int64_t r0 = 4 * (q4 * ks / ksplit);
+  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sbase = (group * K2W + wave) * K2S;
+
+  for (int x = threadIdx.x; x < 3 * BUF; x += NT) lds[x] = (__bf16)0.0f;  // columns >= ldp read as 0
+
+  const int rowbytes = (int)ldp * 2;  // <= 1 KiB for NTC <= 32: one DMA piece per row
+  auto dma_row = [&](const __bf16* src_row, __bf16* dst_row) {
+    const int off = 16 * lane;
+    if (off < rowbytes)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(reinterpret_cast<const char*>(src_row) + off),
+                                       reinterpret_cast<void*>(dst_row), 16, 0, 0);
+  };
+  auto dma_chunk = [&](int64_t c0, __bf16* buf) {  // RPW instructions per wave
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave + K2W * q;
+      dma_row(panel + (c0 + rr) * ldp, buf + rr * STRIDE);
+    }
+  };
+
+  // fragment base of this lane: rows 8g + q (and + 4), columns 4p..4p+3 of each 16-column block
+  const int lb = (8 * (lane >> 4) + ((lane & 15) >> 2)) * STRIDE + 4 * (lane & 3);
+  // slot descriptors are wave-uniform (sbase depends on the wave only): SGPRs, and the needed tiles as one
+  // scalar bit mask, so the 160 accumulator VGPRs keep the vector file to themselves
+  int2 spv[K2S];
+  unsigned long long needm = 0;  // 4 K2S <= 64 bits
+#pragma unroll
+  for (int s = 0; s < K2S; ++s) {
+    int2 sp = supers[sbase + s];
+    sp.x = __builtin_amdgcn_readfirstlane(sp.x);
+    sp.y = __builtin_amdgcn_readfirstlane(sp.y);
+    spv[s] = sp;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int I = 2 * sp.x + (t >> 1), J = 2 * (sp.y & 0xFF) + (t & 1);
+      if (sp.x >= 0 && I <= J && J < NTC && !k2_tile_skip(sp, t)) needm |= 1ull << (4 * s + t);
+    }
+  }
+  flt4 acc[K2S][4];
+#pragma unroll
+  for (int s = 0; s < K2S; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[s][t] = flt4{0.f, 0.f, 0.f, 0.f};
+
+  auto mfma_chunk = [&](const __bf16* cur) {
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 32) {
+#pragma unroll
+      for (int s = 0; s < K2S; ++s) {
+        const int2 sp = spv[s];
+        const bool live = sp.x >= 0;
+        const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * (sp.y & 0xFF), 2 * (sp.y & 0xFF) + 1};
+        bf16x8 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int b = live && blk[u] < NTC ? blk[u] : 0;  // every lane reads (EXEC all ones)
+          x[u] = k2_frag_tr(cur + kk * STRIDE + lb + 16 * b, STRIDE);
+        }
+        constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if ((needm >> (4 * s + t)) & 1ull)
+            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[AB[t][0]], x[AB[t][1]], acc[s][t], 0, 0, 0);
+      }
+    }
+  };
+
+  const int64_t nfull = (r1 - r0) / KC;
+  __syncthreads();  // LDS zeroed (no DMA in flight yet)
+  __bf16* b0 = lds;
+  __bf16* b1 = lds + BUF;
+  __bf16* b2 = lds + 2 * BUF;
+  if (nfull > 0) dma_chunk(r0, b0);
+  if (nfull > 1) {
+    dma_chunk(r0 + KC, b1);
+    k2_wait_vm<RPW>();  // chunk 0 landed (chunk 1 in flight)
+  } else {
+    k2_wait_vm<0>();
+  }
+  k2_barrier();
+  for (int64_t c = 0; c < nfull; ++c) {
+    const bool pre = c + 2 < nfull;
+    if (pre) dma_chunk(r0 + (c + 2) * KC, b2);
+    mfma_chunk(b0);
+    if (pre) k2_wait_vm<RPW>();  // chunk c + 1 landed, chunk c + 2 stays in flight
+    else k2_wait_vm<0>();
+    k2_barrier();
+    __bf16* t = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = t;
+  }
+  if (r0 + nfull * KC < r1) {  // the partial last chunk into b0 (its last reads retired at the barrier above)
+    const int64_t c0 = r0 + nfull * KC;
+    const int valid = (int)(r1 - c0);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave + K2W * q;
+      __bf16* dst = b0 + rr * STRIDE;
+      if (rr < valid) {
+        dma_row(panel + (c0 + rr) * ldp, dst);
+      } else {
+        for (int x = 16 * lane; x < rowbytes; x += 16 * 64)
+          *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst) + x) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    k2_wait_vm<0>();
+    k2_barrier();
+    mfma_chunk(b0);
+  }
+#pragma unroll
+  for (int s = 0; s < K2S; ++s) {
+    if (spv[s].x < 0) continue;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
