@@ -243,9 +243,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step device times from HIP events recorded on the launch stream between the steps (no host
+    # synchronisation inside the timed region): the warm-up evidence VERDICT r2 asked for, not the value
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    marks[0].record(stream)
+    for i in range(args.steps):
         step()
+        marks[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -282,6 +287,13 @@ def main():
                 "avg_launch_ms": round(ms[1], 5)}
 
     ms_step = elapsed / args.steps * 1e3
+    per_step = np.array([marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)])
+    q = max(1, args.steps // 4)
+    step_stats = {"min_ms": round(float(per_step.min()), 5), "median_ms": round(float(np.median(per_step)), 5),
+                  "max_ms": round(float(per_step.max()), 5),
+                  "first_quartile_mean_ms": round(float(per_step[:q].mean()), 5),
+                  "last_quartile_mean_ms": round(float(per_step[-q:].mean()), 5),
+                  "source": "HIP events on the launch stream between consecutive timed steps (rank 0)"}
     # step-level floor: the bytes the step must move (inputs + panel written by K1 and read back by K2; Gram-only
     # chunks may stay on-die and are not counted) at HBM peak, and the Gram flops at the MFMA peak
     step_bytes = N * (in_b + (0 if args.gram_only else 2 * panel_b))
@@ -302,7 +314,10 @@ def main():
                        "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
                    "robot": args.robot, "samples_per_gpu": N, "total_samples_per_step": total_per_step,
                    "nv": nv, "W": W, "parallelism": f"dp{world}",
-                   "exchange": exchange_name},
+                   "exchange": exchange_name,
+                   "timed_region": ("K1 + K2 per panel chunk + K3 (Gram-only)" if args.gram_only else "K1 + K2 + K3")
+                   + ", HBM-resident inputs and outputs" + (", + the Gram all-reduce" if world > 1 else "")},
+        "step_times": step_stats,
         "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
         "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},

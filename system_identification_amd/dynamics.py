@@ -42,7 +42,22 @@ def _axis_rotation(axis: np.ndarray, ang: np.ndarray) -> np.ndarray:
 
 
 def _mv(R, x):
-    return np.einsum("nij,nj->ni", R, x)
+    """Batched 3x3 matrix-vector products, written out (np.einsum on 3x3 blocks cost 3/4 of a G1 1M synthesis)."""
+    return R[:, :, 0] * x[:, None, 0] + R[:, :, 1] * x[:, None, 1] + R[:, :, 2] * x[:, None, 2]
+
+
+def _mtv(R, x):
+    """Batched R^T x."""
+    return R[:, 0, :] * x[:, 0, None] + R[:, 1, :] * x[:, 1, None] + R[:, 2, :] * x[:, 2, None]
+
+
+def _mm(A, B):
+    """Batched 3x3 products A B (either operand may be a single 3x3 matrix)."""
+    A = np.asarray(A)
+    B = np.asarray(B)
+    a = (lambda k: A[:, :, k, None]) if A.ndim == 3 else (lambda k: A[None, :, k, None])
+    b = (lambda k: B[:, None, k, :]) if B.ndim == 3 else (lambda k: B[None, None, k, :])
+    return a(0) * b(0) + a(1) * b(1) + a(2) * b(2)
 
 
 def inverse_dynamics(model: Model, q: np.ndarray, dq: np.ndarray, ddq: np.ndarray) -> np.ndarray:
@@ -70,7 +85,7 @@ def inverse_dynamics(model: Model, q: np.ndarray, dq: np.ndarray, ddq: np.ndarra
             if par != 0:
                 raise NotImplementedError("free-flyer only as the root joint")
             Rb = _quat_to_matrix(q[:, iq + 3:iq + 7])
-            R[i] = np.einsum("ij,njk->nik", model.placements_R[i], Rb)
+            R[i] = _mm(model.placements_R[i], Rb)
             p[i] = q[:, iq:iq + 3] + model.placements_t[i]
             vl, wl = dq[:, iv:iv + 3], dq[:, iv + 3:iv + 6]
             al, dwl = ddq[:, iv:iv + 3], ddq[:, iv + 3:iv + 6]
@@ -80,8 +95,8 @@ def inverse_dynamics(model: Model, q: np.ndarray, dq: np.ndarray, ddq: np.ndarra
             ao[i] = _mv(R[i], al + np.cross(wl, vl))
         else:
             ax = model.axes[i]
-            Rpl = np.einsum("nij,jk->nik", R[par], model.placements_R[i])
-            R[i] = np.einsum("nij,njk->nik", Rpl, _axis_rotation(ax, q[:, iq]))
+            Rpl = _mm(R[par], model.placements_R[i])
+            R[i] = _mm(Rpl, _axis_rotation(ax, q[:, iq]))
             r = _mv(R[par], np.broadcast_to(model.placements_t[i], (N, 3)))
             p[i] = p[par] + r
             u = _mv(Rpl, np.broadcast_to(ax, (N, 3)))
@@ -97,7 +112,7 @@ def inverse_dynamics(model: Model, q: np.ndarray, dq: np.ndarray, ddq: np.ndarra
         c = _mv(R[i], np.broadcast_to(Y.lever, (N, 3)))  # CoM offset from origin, world
         ac = ao[i] + np.cross(dw[i], c) + np.cross(w[i], np.cross(w[i], c))
         F = Y.mass * (ac - g)
-        Iw = np.einsum("nij,jk,nlk->nil", R[i], Y.inertia_c, R[i])
+        Iw = _mm(_mm(R[i], Y.inertia_c), np.swapaxes(R[i], 1, 2))
         Nc = _mv(Iw, dw[i]) + np.cross(w[i], _mv(Iw, w[i]))
         fsub[i] = F
         nsub[i] = Nc + np.cross(c, F)
@@ -110,8 +125,8 @@ def inverse_dynamics(model: Model, q: np.ndarray, dq: np.ndarray, ddq: np.ndarra
     for i in range(1, nj):
         iv = model.idx_v[i]
         if model.jtypes[i] == JOINT_FREEFLYER:
-            tau[:, iv:iv + 3] = np.einsum("nji,nj->ni", R[i], fsub[i])
-            tau[:, iv + 3:iv + 6] = np.einsum("nji,nj->ni", R[i], nsub[i])
+            tau[:, iv:iv + 3] = _mtv(R[i], fsub[i])
+            tau[:, iv + 3:iv + 6] = _mtv(R[i], nsub[i])
         else:
-            tau[:, iv] = np.einsum("ni,ni->n", axw[i], nsub[i])
+            tau[:, iv] = (axw[i] * nsub[i]).sum(axis=1)
     return tau

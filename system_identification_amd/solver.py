@@ -121,6 +121,23 @@ def pullback_metric(phi_prior_link):
     return M
 
 
+def gram_data_term(G, g, btb):
+    """The Gram form of the data term of solver.py:186-190: sum_squares(A x - b) == ‖R x‖² - 2 gᵀx + bᵀb for
+    G = AᵀA, g = Aᵀb, with R = diag(sqrt(max(w, 0))) Vᵀ from the eigendecomposition G = V diag(w) Vᵀ (the
+    clip drops the rounding-level negative eigenvalues of a PSD Gram).  Returns (R, g, btb): the W x W factor
+    that CVXPY sees instead of the N·nv x W stacked matrix, and the linear / constant terms."""
+    G = np.asarray(G, dtype=np.float64)
+    w, V = np.linalg.eigh(0.5 * (G + G.T))
+    R = (V * np.sqrt(np.clip(w, 0.0, None))).T
+    return R, np.asarray(g, dtype=np.float64), float(btb)
+
+
+def gram_data_value(R, g, btb, x):
+    """The value of the data term for a numeric x (what CVXPY minimises, evaluated with numpy)."""
+    Rx = R @ np.asarray(x, dtype=np.float64)
+    return float(Rx @ Rx - 2.0 * (g @ x) + btb)
+
+
 def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_type):  # pragma: no cover
     import cvxpy as cp
     nx = s._nx
@@ -173,8 +190,7 @@ def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_typ
         else:
             x = phi
             G, g = G[:nx, :nx], g[:nx]
-        w, V = np.linalg.eigh(G)
-        R = (V * np.sqrt(np.clip(w, 0, None))).T
+        R, g, btb = gram_data_term(G, g, btb)
         err = cp.sum_squares(R @ x) - 2 * g @ x + btb
     prob = cp.Problem(cp.Minimize(0.5 * err / s._num_samples + lambda_reg * reg), cons)
     prob.solve(solver=cp.MOSEK, mosek_params={"MSK_IPAR_INTPNT_SOLVE_FORM": "MSK_SOLVE_PRIMAL",

@@ -6,7 +6,11 @@
   every stacked array is compared with the C oracle on the same filtered arrays (and a slice with the numpy
   oracle), at north_star's 1e-6.
 * config 4's per-GPU shard: Spot 25k (200k / 8) full outputs, through the device and the host entry points.
+* config 4 whole on one GPU: Spot 200k full outputs (4.5 GB panel): sampled C-oracle rows, Gram ==
+  panelᵀ·panel, and Gram == the sum of the 8 contiguous shard Grams the 8-GPU all-reduce adds.
 * config 5's per-GPU share: G1 125k Gram-only in f64 / f32 / bf16 (1M samples / 8 GPUs).
+* config 5 whole on one GPU: G1 1M Gram-only in f64 (== the sum of its 8 shard Grams, a sampled subset
+  against the oracle's Gram) and in f32 / bf16 (errors against f64 reported).
 * launch state: concurrent launches on two streams, a rejected launch, a corrupted counter."""
 import numpy as np
 import pytest
@@ -100,6 +104,106 @@ def test_config4_shard_full_outputs(robot, N):
     rows = np.concatenate([np.arange(s * nv, (s + 1) * nv) for s in idx])
     out = {k: host[k][rows] for k in ("Y_proj", "tau_proj", "B_v", "B_c")}
     check_stacked_vs_oracle(model, out, o, sub)
+
+
+def _shard_gram_sum(e, din, N, world, gram_only, prec="f64"):
+    """The Grams of the `world` contiguous shards (distributed.shard_range), summed in rank order: what the
+    all-reduce of BASELINE configs 4 / 5 adds up on 8 GPUs."""
+    import torch
+    from system_identification_amd.distributed import shard_range
+    total = None
+    for r in range(world):
+        s0, s1 = shard_range(N, r, world)
+        n = s1 - s0
+        if gram_only:
+            b = e.alloc_gram_device(n)
+            e.build_gram_device(din[:, s0:s1], n, b, precision=prec)
+        else:
+            b = e.alloc_device(n, EMIT_ALL)
+            e.build_device(din[:, s0:s1], n, EMIT_ALL, b)
+        torch.cuda.synchronize()
+        g = b["gram"].cpu().numpy()
+        total = g if total is None else total + g
+        del b
+    return total
+
+
+def test_config4_spot_200k_whole():
+    """BASELINE config 4 (Spot 200k) whole on one GPU, full outputs: sampled rows against the C oracle at
+    1e-6, Gram == panelᵀ·panel (device fp64 GEMM), and Gram == the sum of the 8 contiguous shard Grams to
+    1e-12 -- the exact algebra the 8-GPU all-reduce relies on."""
+    import torch
+    model = load_robot("spot")
+    e = Engine(model)
+    N = 200000
+    d = generate(model, N, config_index=3)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_device(N, EMIT_ALL)
+    e.build_device(din, N, EMIT_ALL, bufs)
+    torch.cuda.synchronize()
+    G = bufs["gram"].cpu().numpy()
+    assert np.array_equal(G, G.T)
+    P = bufs["panel"][:, : e.panel_cols]
+    Gref = (P.T @ P).cpu().numpy()
+    err_pp = rel(G, Gref)
+    parts = _shard_gram_sum(e, din, N, 8, gram_only=False)
+    err_sh = rel(parts, G)
+    print(f"Spot 200k: Gram vs panel^T panel {err_pp:.2e}, vs the sum of 8 shard Grams {err_sh:.2e}")
+    assert err_pp < 1e-12 and err_sh < 1e-12
+    idx = np.sort(np.random.default_rng(4).choice(N, 256, replace=False))
+    nv = model.nv
+    rows = torch.from_numpy(np.concatenate([np.arange(s * nv, (s + 1) * nv) for s in idx])).cuda()
+    panel_rows = bufs["panel"].index_select(0, rows).cpu().numpy()
+    del bufs, P
+    sub = [np.ascontiguousarray(d[k][:, idx]) for k in CH]
+    o = COracle(model).build(*sub, nthreads=8, gram=False)
+    wy, nj, W = e.wy, e.nj, e.w
+    out = {"Y_proj": panel_rows[:, :wy], "B_v": panel_rows[:, wy:wy + nj], "B_c": panel_rows[:, wy + nj:W],
+           "tau_proj": panel_rows[:, W]}
+    check_stacked_vs_oracle(model, out, o, sub)
+
+
+def test_config5_g1_1m_whole_gram_only():
+    """BASELINE config 5 (G1 1M) whole on one GPU, Gram-only: f64 == the sum of the 8 shard Grams (1e-12), a
+    sampled subset's Gram against the oracle (1e-6); f32 / bf16 at 1M with their normwise errors against f64
+    printed (reported, not gated: north_star), and each reduced precision also summed over the 8 shards."""
+    import torch
+    model = load_robot("g1_29dof")
+    e = Engine(model)
+    N = 1000000
+    d = generate(model, N, config_index=5)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    G = {}
+    for prec in ("f64", "f32", "bf16"):
+        b = e.alloc_gram_device(N)
+        e.build_gram_device(din, N, b, precision=prec)
+        torch.cuda.synchronize()
+        G[prec] = b["gram"].cpu().numpy()
+        del b
+    G64 = G["f64"]
+    assert np.array_equal(G64, G64.T)
+    err_sh = rel(_shard_gram_sum(e, din, N, 8, gram_only=True), G64)
+    w = np.linalg.eigvalsh(G64)
+    assert w.min() >= -1e-10 * w.max()
+    idx = np.sort(np.random.default_rng(5).choice(N, 96, replace=False))
+    sub = [np.ascontiguousarray(d[k][:, idx]) for k in CH]
+    o = COracle(model).build(*sub, nthreads=8, stacked=False)
+    dsub = torch.from_numpy(channel_block(dict(zip(CH, sub)))).cuda()
+    b = e.alloc_gram_device(len(idx))
+    e.build_gram_device(dsub, len(idx), b)
+    torch.cuda.synchronize()
+    Gs = b["gram"].cpu().numpy()
+    W = e.w
+    err_o = max(rel(Gs[:W, :W], o["gram"]), rel(Gs[:W, W], o["Atb"]))
+    nrm = np.linalg.norm(G64)
+    errs = {p: float(np.linalg.norm(G[p] - G64) / nrm) for p in ("f32", "bf16")}
+    sh = {p: rel(_shard_gram_sum(e, din, N, 8, gram_only=True, prec=p), G[p]) for p in ("f32", "bf16")}
+    print(f"G1 1M Gram-only: f64 vs the sum of 8 shard Grams {err_sh:.2e}, sampled subset vs oracle {err_o:.2e}; "
+          f"normwise error vs f64: f32 {errs['f32']:.2e} bf16 {errs['bf16']:.2e}; "
+          f"shard sums f32 {sh['f32']:.2e} bf16 {sh['bf16']:.2e}")
+    assert err_sh < 1e-12 and err_o < TOL
+    assert errs["f32"] < 1e-5 and errs["bf16"] < 3e-2
+    assert sh["f32"] < 1e-5 and sh["bf16"] < 1e-3
 
 
 def test_host_entry_point_odd_friction_width():

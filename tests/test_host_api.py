@@ -132,3 +132,72 @@ def test_llsq_gram_path_on_real_panel(robot):
     assert np.linalg.norm(ps - pg) <= 1e-6 * np.linalg.norm(ps)
     # the Gram solution does not blow up along the unidentifiable directions
     assert np.linalg.norm(phi_g) <= 1.5 * np.linalg.norm(phi_s)
+
+
+def test_prior_table_matches_the_reference_printed_output(capsys):
+    """The one output the reference ships (demo/RUN_DEMO.md:10-21): the 'A priori' column that
+    print_inertial_params (src/sys_identification.py:439-490) prints for Spot's front_left_hip, from
+    get_phi_prior (:297-322).  Pins the host prior and the table format, not the hot path."""
+    import json
+    import os
+    from system_identification_amd.sys_identification import SystemIdentification
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "run_demo_front_left_hip.json")))
+    s = SystemIdentification("spot")
+    prior = s.get_phi_prior()
+    s.print_inertial_params(prior, prior)
+    lines = capsys.readouterr().out.splitlines()
+    i = next(k for k, ln in enumerate(lines) if f'"{fx["link"]}"' in ln)
+    assert lines[i + 1] == fx["header"]
+    for k, (label, value) in enumerate(fx["a_priori"]):
+        cells = lines[i + 2 + k].split("|")
+        assert cells[1].strip() == label and cells[2].strip() == value, (label, cells)
+        assert len(cells[2]) == 13  # the reference's 13-wide right-aligned cell
+
+
+@pytest.mark.parametrize("robot,friction", [("spot", True), ("solo12", False)])
+def test_gram_form_data_term_equals_stacked(robot, friction):
+    """f1: the data term CVXPY minimises in the Gram form, ‖R x‖² - 2 gᵀx + bᵀb with R from the
+    clipped eigendecomposition of G (solver.gram_data_term), equals the reference's sum_squares(A x - b)
+    (src/solver.py:186-190) on the oracle's stacked A for random x, scaled by 1/(2 rows) as in :190."""
+    from oracle.ref_c import COracle
+    from system_identification_amd.model import load_robot
+    from system_identification_amd.solver import gram_data_term, gram_data_value
+    from system_identification_amd.synthetic import generate
+    model = load_robot(robot)
+    d = generate(model, 300, config_index=4)
+    o = COracle(model).build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"])
+    A = np.hstack([o["Y_proj"], o["B_v"], o["B_c"]]) if friction else o["Y_proj"]
+    b = o["tau_proj"]
+    W = A.shape[1]
+    G, g = (o["gram"], o["Atb"]) if friction else (o["gram"][:W, :W], o["Atb"][:W])
+    R, g, btb = gram_data_term(G, g, o["btb"])
+    rows = A.shape[0]
+    assert rows == 300 * model.nv
+    rng = np.random.default_rng(7)
+    for scale in (1e-3, 1.0, 1e2):
+        x = rng.standard_normal(W) * scale
+        ref_val = 0.5 * float(np.sum((A @ x - b) ** 2)) / rows
+        val = 0.5 * gram_data_value(R, g, btb, x) / rows
+        assert abs(val - ref_val) <= 1e-10 * abs(ref_val), (scale, val, ref_val)
+
+
+def test_gram_llsq_noise_floor_is_pinned():
+    """the Gram-form llsq cuts eigenvalues at n·eps·w_max (directions with sigma below ~sqrt(n eps)
+    sigma_max), where the stacked SVD keeps everything above 1e-15 sigma_max (src/solver.py:37).  A direction at
+    1e-8 sigma_max is identified by the stacked path and dropped by the Gram path (its eigenvalue 1e-16 w_max is
+    below the squaring's rounding floor), while one at 1e-5 sigma_max is identified by both."""
+    rng = np.random.default_rng(11)
+    m, n = 400, 20
+    U, _ = np.linalg.qr(rng.standard_normal((m, n)))
+    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    sig = np.logspace(0, -3, n)
+    sig[-2], sig[-1] = 1e-5, 1e-8
+    Y = (U * sig) @ V.T
+    c = np.ones(n)
+    t = (U * sig) @ c  # tau = Y V c: every direction carries a unit coefficient
+    phi_s = Solver(Y, t, 2, np.zeros(n), 1.0, None).solve_llsq_svd()
+    ne = {"gram": Y.T @ Y, "Atb": Y.T @ t, "btb": float(t @ t), "num_rows": m}
+    phi_g = Solver.from_normal_equations(ne, 2, np.zeros(n), 1.0, None, friction=False).solve_llsq_svd()
+    cs, cg = V.T @ phi_s, V.T @ phi_g
+    assert abs(cs[-2] - 1.0) < 1e-6 and abs(cg[-2] - 1.0) < 1e-3   # sigma = 1e-5 sigma_max: both
+    assert abs(cs[-1] - 1.0) < 1e-3 and abs(cg[-1]) < 1e-6          # sigma = 1e-8: stacked only
