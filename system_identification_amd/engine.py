@@ -111,20 +111,35 @@ def _ptr(a):
 
 
 PINNED_MIN_BYTES = 8 << 20
+PINNED_MAX_BYTES = 1 << 30  # larger outputs: pageable (the C side page-locks them for the copy, host_copy)
 
 
 def host_empty(shape, dtype=np.float64):
-    """An output array for the host entry points.  Large outputs live in page-locked memory from PyTorch's
-    caching host allocator: the DMA engine writes them at full PCIe rate, and a repeated call reuses blocks
-    that are already pinned and paged in (a fresh np.empty pays one page fault per 4 KiB on first touch, which
-    cost more than the copy itself: ~23 ms vs ~7 ms for Spot 20k's 374 MB Y_proj).  The caller gets a plain
-    numpy array; the memory returns to the allocator's cache when the array is dropped."""
+    """An output array for the host entry points.  Outputs of 8 MiB .. 1 GiB live in page-locked memory from
+    PyTorch's caching host allocator: the DMA engine writes them at full PCIe rate, and a repeated call reuses
+    blocks that are already pinned and paged in (a fresh np.empty pays one page fault per 4 KiB on first touch,
+    which cost more than the copy itself: ~23 ms vs ~7 ms for Spot 20k's 374 MB Y_proj).
+
+    That allocator rounds every block up to a power of two and keeps it cached, page-locked, after the array
+    is dropped (release_pinned_cache() returns it to the OS).  Hence the 1 GiB cap: a larger output (e.g. a
+    G1 full-output call's ~8 GB Y_proj) is plain np.empty, and sysid_build page-locks it only for the
+    duration of its copy (hipHostRegister).  A failed pinned allocation also falls back to np.empty."""
     nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
-    if nbytes < PINNED_MIN_BYTES:
+    if nbytes < PINNED_MIN_BYTES or nbytes > PINNED_MAX_BYTES:
         return np.empty(shape, dtype=dtype)
     import torch
     tdt = {np.dtype(np.float64): torch.float64, np.dtype(np.float32): torch.float32}[np.dtype(dtype)]
-    return torch.empty(tuple(shape), dtype=tdt, pin_memory=True).numpy()
+    try:
+        return torch.empty(tuple(shape), dtype=tdt, pin_memory=True).numpy()
+    except RuntimeError:
+        return np.empty(shape, dtype=dtype)
+
+
+def release_pinned_cache():
+    """Return the page-locked blocks cached by host_empty (PyTorch's caching host allocator) to the OS;
+    arrays still alive keep theirs."""
+    import torch
+    torch._C._host_emptyCache()
 
 
 def _require_gpu():
