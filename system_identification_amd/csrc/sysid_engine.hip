@@ -50,6 +50,9 @@ struct sysid_engine {
   unsigned long long* d_work = nullptr;  // K1 sample counter of the host-API paths (engine-owned buffers)
   int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4, k1_variant = 0;
   size_t k1_lds = 0;
+  // K1 of the Gram-only nullspace mode (CMP instantiations, always the plain layout): its own launch shape
+  int k1c_variant = 0, k1c_waves = 4, k1c_blocks_per_cu = 1, k1c_wave_dbl = 0;
+  size_t k1c_lds = 0;
   // K2/K3 Gram tiling
   int ntc = 0;
   // super-tile deal per Gram arithmetic (0 f64, 1 f32, 2 bf16): each kernel's waves x slots per wave
@@ -94,12 +97,9 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 
 // K2 split-K: one workgroup per CU and super-tile group; wide Grams (>= 16 tile columns, small row
 // chunks) run two workgroups per CU (measured: G1 K2 -11%, Spot unchanged net of the larger K3).
-#ifndef SYSID_K2_DMA_NARROW
-#define SYSID_K2_DMA_NARROW 0  // experiment: narrow Grams (<= 10 tile columns) on the DMA kernel, 16-row chunks, 2 WG/CU
-#endif
 int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
   // the bf16 kernel's large chunks take most of a CU's LDS: one workgroup per CU
-  const int mult = (e->ntc >= 16 || (SYSID_K2_DMA_NARROW && e->ntc <= 10)) && prec != 2 ? 2 : 1;
+  const int mult = e->ntc >= 16 && prec != 2 ? 2 : 1;
   int ks = std::max(1, mult * e->cus / std::max(1, e->k2d[prec].ngroups));
   const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
@@ -122,24 +122,15 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
 // K1 instantiations: chain slots x compile-time nv x samples per wave.  Quadrupeds (nv = 18) run two
 // samples per wave; anything else one, with nv read at run time (a compile-time nv = 35 for the humanoid
 // ran 1.8x slower, its unrolled serial phases being heavier than the saved address arithmetic).
-#ifndef SYSID_K1_SPW_QUAD
-#define SYSID_K1_SPW_QUAD 2
-#endif
-#ifndef SYSID_K1_SPW_GEN
-#define SYSID_K1_SPW_GEN 1
-#endif
+constexpr int SYSID_K1_SPW_QUAD = 2, SYSID_K1_SPW_GEN = 1;
 // Chain slots of the nv = 18 kernel: the quadrupeds' legs are 3 revolute joints deep (3 measured 2% faster
 // than 4 on Spot: no dead slot in the column phase).
-#ifndef SYSID_K1_QCH
-#define SYSID_K1_QCH 3
-#endif
+constexpr int SYSID_K1_QCH = 3;
 enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16, K1_C12P, K1_C16P };  // ...P: the P-overlay layout (wave_layout pov)
 int k1_pov_variant(int variant) { return variant == K1_C12 ? K1_C12P : variant == K1_C16 ? K1_C16P : -1; }
 bool k1_is_pov(int variant) { return variant == K1_C12P || variant == K1_C16P; }
-#ifndef SYSID_K1_C12
-#define SYSID_K1_C12 1  // a 12-slot instantiation for chains of 5..12 revolute joints (G1: 10)
-#endif
-int k1_chain_slots(int maxch) { return maxch <= 4 ? 4 : (SYSID_K1_C12 && maxch <= 12) ? 12 : 16; }
+// a 12-slot instantiation for chains of 5..12 revolute joints (G1: 10; -2.8% against 16 slots)
+int k1_chain_slots(int maxch) { return maxch <= 4 ? 4 : maxch <= 12 ? 12 : 16; }
 
 // maxch: the longest revolute chain.  The nv = 18 kernel unrolls SYSID_K1_QCH chain slots.
 int k1_variant(int maxch, int nv, int nbody) {
@@ -153,15 +144,20 @@ int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : SYS
 // wave_layout's `hw`: lanes per sample of the compile-time-nv kernel (P over Z), 0 for the others.
 int k1_layout_hw(int variant) { return variant == K1_C4_NV18 ? 64 / k1_spw(variant) : 0; }
 
-const void* k1_fn(int variant) {
+// The instantiation of a variant for a panel element type (prec: 0 f64, 1 f32, 2 bf16).
+template <typename OutT>
+const void* k1_fn_t(int variant) {
   switch (variant) {
-    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, double>);
-    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, double>);
-    case K1_C12: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, double>);
-    case K1_C12P: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, double, 1>);
-    case K1_C16P: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, double, 1>);
-    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, double>);
+    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, OutT>);
+    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT>);
+    case K1_C12: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT>);
+    case K1_C12P: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 1>);
+    case K1_C16P: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 1>);
+    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT>);
   }
+}
+const void* k1_fn(int variant, int prec = 0) {
+  return prec == 0 ? k1_fn_t<double>(variant) : prec == 1 ? k1_fn_t<float>(variant) : k1_fn_t<__bf16>(variant);
 }
 
 // Panel element of each Gram arithmetic: 0 = f64 (parity; every stacked output), 1 = f32, 2 = bf16 (the
@@ -171,69 +167,92 @@ size_t prec_bytes(int prec) { return prec == 0 ? 8 : prec == 1 ? 4 : 2; }
 // Gram arithmetic selected by the flags: 0 = f64 (parity), 1 = f32 MFMA, 2 = bf16 MFMA (error reported).
 int gram_prec(uint32_t flags) { return (flags & SYSID_GRAM_BF16) ? 2 : (flags & SYSID_GRAM_F32) ? 1 : 0; }
 
-template <typename OutT>
-void k1_launch_typed(sysid_engine* e, dim3 g1, dim3 b1, hipStream_t st, const K1Params& kp, const double* d_in,
-                     int64_t N, int64_t ld, OutT* d_panel, int64_t ld_panel, unsigned long long* work, double* dbg) {
-  switch (e->k1_variant) {
-    case K1_C4_NV18:
-      hipLaunchKernelGGL((k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, OutT>), g1, b1, e->k1_lds, st, kp,
-                         e->d_mimg, d_in, N, ld, d_panel, ld_panel, work, dbg);
-      break;
-    case K1_C4:
-      hipLaunchKernelGGL((k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg, d_in,
-                         N, ld, d_panel, ld_panel, work, dbg);
-      break;
-    case K1_C12:
-      hipLaunchKernelGGL((k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
-                         d_in, N, ld, d_panel, ld_panel, work, dbg);
-      break;
+template <typename OutT, int CMP = 0>
+void k1_launch_typed(sysid_engine* e, int variant, dim3 g1, dim3 b1, size_t lds, hipStream_t st, const K1Params& kp,
+                     const double* d_in, int64_t N, int64_t ld, OutT* d_panel, int64_t ld_panel,
+                     unsigned long long* work, double* dbg, int* rcount) {
+#define SYSID_K1_LAUNCH(MAXCH, NVC, SPW, POV)                                                                      \
+  hipLaunchKernelGGL((k1_regressor_panel<MAXCH, NVC, SPW, OutT, POV, CMP>), g1, b1, lds, st, kp, e->d_mimg, d_in, N, \
+                     ld, d_panel, ld_panel, work, dbg, rcount)
+  switch (variant) {
+    case K1_C4_NV18: SYSID_K1_LAUNCH(SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, 0); break;
+    case K1_C4: SYSID_K1_LAUNCH(4, 0, SYSID_K1_SPW_GEN, 0); break;
+    case K1_C12: SYSID_K1_LAUNCH(12, 0, SYSID_K1_SPW_GEN, 0); break;
+    case K1_C16: SYSID_K1_LAUNCH(16, 0, SYSID_K1_SPW_GEN, 0); break;
     case K1_C12P:
-      hipLaunchKernelGGL((k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
-                         d_in, N, ld, d_panel, ld_panel, work, dbg);
+      if constexpr (!CMP) SYSID_K1_LAUNCH(12, 0, SYSID_K1_SPW_GEN, 1);
       break;
     case K1_C16P:
-      hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 1>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
-                         d_in, N, ld, d_panel, ld_panel, work, dbg);
+      if constexpr (!CMP) SYSID_K1_LAUNCH(16, 0, SYSID_K1_SPW_GEN, 1);
       break;
-    default:
-      hipLaunchKernelGGL((k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT>), g1, b1, e->k1_lds, st, kp, e->d_mimg,
-                         d_in, N, ld, d_panel, ld_panel, work, dbg);
   }
+#undef SYSID_K1_LAUNCH
 }
 
+// The nullspace-mode instantiation of a variant (OutT of the Gram arithmetic), for the occupancy query.
+const void* k1_fn_cmp(int variant, int prec) {
+#define SYSID_K1_FN(MAXCH, NVC, SPW)                                                                              \
+  (prec == 0   ? reinterpret_cast<const void*>(k1_regressor_panel<MAXCH, NVC, SPW, double, 0, 1>)                \
+   : prec == 1 ? reinterpret_cast<const void*>(k1_regressor_panel<MAXCH, NVC, SPW, float, 0, 1>)                 \
+               : reinterpret_cast<const void*>(k1_regressor_panel<MAXCH, NVC, SPW, __bf16, 0, 1>))
+  switch (variant) {
+    case K1_C4_NV18: return SYSID_K1_FN(SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD);
+    case K1_C4: return SYSID_K1_FN(4, 0, SYSID_K1_SPW_GEN);
+    case K1_C12: return SYSID_K1_FN(12, 0, SYSID_K1_SPW_GEN);
+    default: return SYSID_K1_FN(16, 0, SYSID_K1_SPW_GEN);
+  }
+#undef SYSID_K1_FN
+}
+
+// cmp: the Gram-only nullspace mode (rcount: its per-sample row counts).
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
-              unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0) {
+              unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0, int cmp = 0,
+              int* rcount = nullptr) {
   K1Params kp = e->kp;
   HIP_TRY(e, hipMemsetAsync(work, 0, WORK_BYTES, st));
   if (full) {
     kp.full = 1;
     kp.in_rows = e->in_lds;
   }
-  const int spw = k1_spw(e->k1_variant);
+  const int variant = cmp ? e->k1c_variant : e->k1_variant;
+  const int waves = cmp ? e->k1c_waves : e->k1_waves;
+  const int bpc = cmp ? e->k1c_blocks_per_cu : e->k1_blocks_per_cu;
+  const size_t lds = cmp ? e->k1c_lds : e->k1_lds;
+  if (cmp) {
+    kp.pov = 0;
+    kp.wave_dbl = e->k1c_wave_dbl;
+  }
+  const int spw = k1_spw(variant);
   kp.rg = k1_row_groups(kp.NJ, 64 / spw);
   kp.out_cols = (int)std::min<int64_t>(ld_panel, prec == 0 ? e->ldp : ld_panel);
   const int64_t waves_needed = (N + spw - 1) / spw;
-  const int64_t cap = (int64_t)e->cus * e->k1_blocks_per_cu;
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + e->k1_waves - 1) / e->k1_waves));
-  const dim3 g1((unsigned)grid), b1(64 * e->k1_waves);
-  if (prec == 0)
-    k1_launch_typed(e, g1, b1, st, kp, d_in, N, ld, static_cast<double*>(d_panel), ld_panel, work, dbg);
-  else if (prec == 1)
-    k1_launch_typed(e, g1, b1, st, kp, d_in, N, ld, static_cast<float*>(d_panel), ld_panel, work, dbg);
-  else
-    k1_launch_typed(e, g1, b1, st, kp, d_in, N, ld, static_cast<__bf16*>(d_panel), ld_panel, work, dbg);
+  const int64_t cap = (int64_t)e->cus * bpc;
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + waves - 1) / waves));
+  const dim3 g1((unsigned)grid), b1(64 * waves);
+#define SYSID_K1_TYPED(CMPV)                                                                                       \
+  if (prec == 0)                                                                                                   \
+    k1_launch_typed<double, CMPV>(e, variant, g1, b1, lds, st, kp, d_in, N, ld, static_cast<double*>(d_panel),     \
+                                  ld_panel, work, dbg, rcount);                                              \
+  else if (prec == 1)                                                                                              \
+    k1_launch_typed<float, CMPV>(e, variant, g1, b1, lds, st, kp, d_in, N, ld, static_cast<float*>(d_panel),       \
+                                 ld_panel, work, dbg, rcount);                                               \
+  else                                                                                                             \
+    k1_launch_typed<__bf16, CMPV>(e, variant, g1, b1, lds, st, kp, d_in, N, ld, static_cast<__bf16*>(d_panel),     \
+                                  ld_panel, work, dbg, rcount);
+  if (cmp) {
+    SYSID_K1_TYPED(1)
+  } else {
+    SYSID_K1_TYPED(0)
+  }
+#undef SYSID_K1_TYPED
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
 
-#ifndef SYSID_K2_KC10
-#define SYSID_K2_KC10 32  // rows per chunk of the register-staged kernel at 10 tile columns (Spot)
-#endif
-#ifndef SYSID_K2_DMA
-#define SYSID_K2_DMA 1  // 1: LDS-DMA staged, three buffers (k2_gram_syrk_dma); 0: register-staged k2_gram_syrk
-#endif
+// rowlist / d_rows: the nullspace mode's gathered rows (k1s_row_list; `rows` is then only the bound the split
+// was sized for): the LDS-DMA kernels for every width and arithmetic.
 int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
-              double* slab, hipStream_t st, int prec) {
+              double* slab, hipStream_t st, int prec, const int* rowlist = nullptr, const int* d_rows = nullptr) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
   const sysid_engine::Deal& D = e->k2d[prec];
@@ -241,45 +260,67 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
   const double* p64 = static_cast<const double*>(d_panel);
   const float* p32 = static_cast<const float*>(d_panel);
   const __bf16* p16 = static_cast<const __bf16*>(d_panel);
+  const bool gather = rowlist != nullptr;
   switch (e->ntc) {
 // f64 / f32 Gram kernels: LDS-DMA staged (three buffers) for wide Grams, register-staged for narrow ones
-// (measured, 20k samples: G1 K2 1.81 -> 1.66 ms with the DMA kernel; Spot 0.202 -> 0.213 ms, so not there).
-#define SYSID_K2_F64(NTC, KC)                                                                                \
-  if constexpr (SYSID_K2_DMA && (NTC >= 16 || (SYSID_K2_DMA_NARROW && NTC <= 10)))                           \
-    hipLaunchKernelGGL((k2_gram_syrk_dma<double, NTC, k2_dma_kc(NTC)>), g2, b2, 0, st, p64, rows, ld_panel,    \
-                       D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);                            \
-  else                                                                                                      \
-    hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, D.d_tiles,       \
-                       D.ngroups, ks, D.nslots, accumulate, slab);
-#define SYSID_K2_F32(NTC, KC) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                   \
-  if constexpr (SYSID_K2_DMA && (NTC >= 16 || (SYSID_K2_DMA_NARROW && NTC <= 10)))                           \
-    hipLaunchKernelGGL((k2_gram_syrk_dma<float, NTC, 2 * k2_dma_kc(NTC)>), g2, b2, 0, st, p32, rows, ld_panel, \
-                       D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);                            \
-  else                                                                                                      \
-    hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, D.d_tiles,    \
-                       D.ngroups, ks, D.nslots, accumulate, slab);
-#define SYSID_K2_CASE(NTC, KC)                                                                               \
-  case NTC:                                                                                                 \
-    if (prec == 0) {                                                                                        \
-      SYSID_K2_F64(NTC, KC)                                                                                 \
-    } else if (prec == 1) {                                                                                 \
-      SYSID_K2_F32(NTC, KC)                                                                                 \
-    } else {                                                                                                \
-      if constexpr (SYSID_K2_BF16_TR && NTC >= 16)                                                          \
-        hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0,  \
-                           st, p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);  \
-      else                                                                                                  \
-        hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st,  \
-                           p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);      \
-    }                                                                                                       \
+// (measured, 20k samples: G1 K2 1.81 -> 1.66 ms with the DMA kernel; Spot 0.202 -> 0.213 ms, so not there);
+// the gathered rows of the nullspace mode always go through the DMA kernels.
+#define SYSID_K2_DMA_LAUNCH(T, P, NTC, KC)                                                                          \
+  if (gather)                                                                                                       \
+    hipLaunchKernelGGL((k2_gram_syrk_dma<T, NTC, KC, true>), g2, b2, 0, st, P, rows, ld_panel, D.d_tiles,         \
+                       D.ngroups, ks, D.nslots, accumulate, slab, rowlist, d_rows);                                 \
+  else                                                                                                              \
+    hipLaunchKernelGGL((k2_gram_syrk_dma<T, NTC, KC>), g2, b2, 0, st, P, rows, ld_panel, D.d_tiles, D.ngroups,    \
+                       ks, D.nslots, accumulate, slab, nullptr, nullptr);
+#define SYSID_K2_F64(NTC, KC)                                                                                      \
+  if constexpr (NTC >= 16) {                                \
+    SYSID_K2_DMA_LAUNCH(double, p64, NTC, k2_dma_kc(NTC))                                                           \
+  } else if (gather) {                                                                                              \
+    hipLaunchKernelGGL((k2_gram_syrk_dma<double, NTC, k2_dma_kc(NTC), true>), g2, b2, 0, st, p64, rows, ld_panel,  \
+                       D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist, d_rows);                      \
+  } else {                                                                                                          \
+    hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, D.d_tiles,             \
+                       D.ngroups, ks, D.nslots, accumulate, slab);                                                  \
+  }
+#define SYSID_K2_F32(NTC, KC) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                        \
+  if constexpr (NTC >= 16) {                                \
+    SYSID_K2_DMA_LAUNCH(float, p32, NTC, 2 * k2_dma_kc(NTC))                                                        \
+  } else if (gather) {                                                                                              \
+    hipLaunchKernelGGL((k2_gram_syrk_dma<float, NTC, 2 * k2_dma_kc(NTC), true>), g2, b2, 0, st, p32, rows,         \
+                       ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist, d_rows);            \
+  } else {                                                                                                          \
+    hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, D.d_tiles,          \
+                       D.ngroups, ks, D.nslots, accumulate, slab);                                                  \
+  }
+#define SYSID_K2_CASE(NTC, KC)                                                                                     \
+  case NTC:                                                                                                       \
+    if (prec == 0) {                                                                                              \
+      SYSID_K2_F64(NTC, KC)                                                                                       \
+    } else if (prec == 1) {                                                                                       \
+      SYSID_K2_F32(NTC, KC)                                                                                       \
+    } else if (gather) {                                                                                          \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC), true>), g2, dim3(64 * K2_BF16_WAVES), 0, \
+                         st, p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist,  \
+                         d_rows);                                                                                 \
+    } else if constexpr (NTC >= 16) {                                                                            \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st,    \
+                         p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, nullptr,      \
+                         nullptr);                                                                                \
+    } else {                                                                                                      \
+      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16,    \
+                         rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);                   \
+    }                                                                                                             \
     break;
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
-    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, SYSID_K2_KC10)
+    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
     SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20)
     SYSID_K2_CASE(15, 20) SYSID_K2_CASE(16, 12) SYSID_K2_CASE(17, 12) SYSID_K2_CASE(18, 12)
     SYSID_K2_CASE(19, 12) SYSID_K2_CASE(20, 12) SYSID_K2_CASE(21, 8) SYSID_K2_CASE(22, 8)
     SYSID_K2_CASE(23, 8) SYSID_K2_CASE(24, 8)
 #undef SYSID_K2_CASE
+#undef SYSID_K2_F64
+#undef SYSID_K2_F32
+#undef SYSID_K2_DMA_LAUNCH
     default:
       return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
   }
@@ -351,12 +392,7 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
 // Chunk panel of ~1 GiB: every K1 launch ends in a tail of partly idle CUs (a G1 wave-step is ~20 us), so few
 // large chunks beat MALL-sized ones (G1 125k bf16 step: 64 MB chunks 11.2 ms, 128 MB 10.3, 256 MB 9.3,
 // 512 MB 8.6, 1 GiB 8.3; profiles/r02_p2).
-size_t gram_chunk_bytes() {
-#ifdef SYSID_EXPERIMENTS
-  if (const char* v = std::getenv("SYSID_GRAM_CHUNK_MB")) return (size_t)std::max(1, std::atoi(v)) << 20;
-#endif
-  return (size_t)1 << 30;
-}
+size_t gram_chunk_bytes() { return (size_t)1 << 30; }
 
 int64_t gram_ld(const sysid_engine* e, int prec) {
   const int64_t m = prec == 0 ? 2 : prec == 1 ? 4 : 8;
@@ -369,29 +405,49 @@ int64_t gram_chunk(const sysid_engine* e, int64_t N, int prec) {
   return std::max<int64_t>(1, std::min(c, N));
 }
 
-// [K1 counter | panel chunk | K2 slabs]
+// Nullspace mode extras: after the claim counters, the live-row total (one 256-byte line) and the segment sums;
+// after the slabs, the per-sample row counts and the row list.
+size_t cmp_head_bytes(int64_t C) { return 256 + align256((size_t)((C + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG) * 4); }
+size_t cmp_tail_bytes(const sysid_engine* e, int64_t C) {
+  return align256((size_t)C * 4) + align256((size_t)C * e->nv * 4);
+}
+
+// [K1 counters | row total, segment sums | panel chunk | K2 slabs | row counts | row list]
 size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
-  const int64_t rows = gram_chunk(e, N, prec) * e->nv;
-  return WORK_BYTES + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) + slab_bytes(e, rows, prec);
+  const int64_t C = gram_chunk(e, N, prec), rows = C * e->nv;
+  return WORK_BYTES + cmp_head_bytes(C) + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) +
+         slab_bytes(e, rows, prec) + cmp_tail_bytes(e, C);
 }
 
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
   return std::max({gram_ws_bytes_prec(e, N, 0), gram_ws_bytes_prec(e, N, 1), gram_ws_bytes_prec(e, N, 2)});
 }
 
-// ev (optional, diagnostics): 2 events per chunk + 2 for K3, recorded around each K1 / K2 / K3 launch.
+// ev (optional, diagnostics): 2 events per chunk + 2 for K3, recorded around each K1 (+ row list) / K2 / K3 launch.
+// Nullspace mode: K1 emits Zᵀ·A, nv - rank(J_c) rows per sample, k1s_seg_sums / k1s_row_list list them and K2
+// gathers them; projector mode: the reference's P·A rows (nv per sample), contiguous.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
+  // rows: nullspace (needs K1's register LU: at most K1_CMP_KMAX contact rows) or projector; by default the
+  // nullspace rows for the f64 / f32 Grams and the projector rows for bf16 (include/sysid.h)
+  const bool want_ns = (flags & SYSID_GRAM_NULLSPACE) ? true : (flags & SYSID_GRAM_PROJECTOR) ? false : prec != 2;
+  const int cmp = want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
                    gram_ws_bytes_prec(e, N, prec));
   if (reinterpret_cast<uintptr_t>(d_ws) & 255) return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
   const int64_t C = gram_chunk(e, N, prec), rows0 = C * e->nv, ldc = gram_ld(e, prec);
+  if (rows0 >= ((int64_t)1 << 31)) return set_err(e, SYSID_E_INVALID, "Gram-only chunk of %lld rows", (long long)rows0);
   auto* work = static_cast<unsigned long long*>(d_ws);
-  char* panel = static_cast<char*>(d_ws) + WORK_BYTES;
+  char* head = static_cast<char*>(d_ws) + WORK_BYTES;
+  int* d_rows = reinterpret_cast<int*>(head);
+  int* rseg = reinterpret_cast<int*>(head + 256);
+  char* panel = head + cmp_head_bytes(C);
   double* slab = reinterpret_cast<double*>(panel + align256((size_t)rows0 * ldc * prec_bytes(prec)));
+  int* rcount = reinterpret_cast<int*>(reinterpret_cast<char*>(slab) + slab_bytes(e, rows0, prec));
+  int* rowlist = reinterpret_cast<int*>(reinterpret_cast<char*>(rcount) + align256((size_t)C * 4));
   const int ks0 = ksplit_for(e, rows0, prec);  // slab_bytes(e, rows0, prec): the slabs fit the workspace
   int rc;
   size_t k = 0;
@@ -401,10 +457,22 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   };
   for (int64_t c0 = 0; c0 < N; c0 += C) {
     const int64_t n = std::min(C, N - c0);
-    if ((rc = mark()) || (rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec)) || (rc = mark()))
+    if ((rc = mark())) return rc;
+    if (cmp) {
+      if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount)))
+        return rc;
+      const unsigned nseg = (unsigned)((n + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG);
+      hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
+      hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, rseg, (int)n, e->nv, rowlist, d_rows);
+      HIP_TRY(e, hipGetLastError());
+    } else if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec))) {
       return rc;
+    }
+    if ((rc = mark())) return rc;
     const int ks = std::min(ks0, ksplit_for(e, n * e->nv, prec));
-    if ((rc = launch_k2(e, panel, n * e->nv, ldc, ks, c0 > 0, slab, st, prec)) != SYSID_OK) return rc;
+    if ((rc = launch_k2(e, panel, n * e->nv, ldc, ks, c0 > 0, slab, st, prec, cmp ? rowlist : nullptr,
+                        cmp ? d_rows : nullptr)) != SYSID_OK)
+      return rc;
   }
   if ((rc = mark())) return rc;
   if ((rc = launch_k3(e, ks0, slab, d_gram, st, prec))) return rc;
@@ -755,20 +823,23 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) {
     int best = -1;
     // layouts: the plain one first (kept on ties), then the P overlay; 8-wave workgroups for one-sample waves
-#ifndef SYSID_K1_POV
-#define SYSID_K1_POV 1
-#endif
     const int v0 = e->k1_variant;
-    for (int ov = 0; ov < (SYSID_K1_POV && pov_ok ? 2 : 1); ++ov) {
+    for (int ov = 0; ov < (pov_ok ? 2 : 1); ++ov) {
       const WLay& wl = ov ? WL1 : WL0;
       const int var = ov ? k1_pov_variant(v0) : v0;
       for (int wv : {8, 4, 2, 1}) {
         if (wv > K1_WAVES && !k1_is_pov(var)) continue;  // 8-wave workgroups: the overlay instantiations only
         const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(var) * wl.total) * sizeof(double);
         if (lds > 160 * 1024) continue;
-        (void)hipFuncSetAttribute(k1_fn(var), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k1_fn(var), 64 * wv, lds) != hipSuccess) nb = 0;
+        // every panel element type's instantiation (the Gram-only f32 / bf16 paths launch their own): the
+        // shape must be resident for each of them
+        int nb = 1 << 30;
+        for (int pr = 0; pr < 3; ++pr) {
+          (void)hipFuncSetAttribute(k1_fn(var, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+          int x = 0;
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k1_fn(var, pr), 64 * wv, lds) != hipSuccess) x = 0;
+          nb = std::min(nb, x);
+        }
         if (nb * wv > best) {
           best = nb * wv;
           e->k1_waves = wv;
@@ -786,10 +857,36 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       sysid_destroy(e);
       return SYSID_E_MODEL;
     }
-    st = hipFuncSetAttribute(k1_fn(e->k1_variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
-#ifdef SYSID_EXPERIMENTS
-    if (const char* v = std::getenv("SYSID_K1_BLOCKS_PER_CU")) e->k1_blocks_per_cu = std::max(1, std::atoi(v));
-#endif
+    for (int pr = 0; pr < 3 && st == hipSuccess; ++pr)
+      st = hipFuncSetAttribute(k1_fn(e->k1_variant, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
+    // the Gram-only nullspace mode: its CMP instantiations of the plain-layout variant, shaped the same way
+    int bestc = -1;
+    e->k1c_variant = v0;
+    for (int wv : {4, 2, 1}) {
+      const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(v0) * WL0.total) * sizeof(double);
+      if (lds > 160 * 1024) continue;
+      int nb = 1 << 30;
+      for (int pr = 0; pr < 3; ++pr) {
+        (void)hipFuncSetAttribute(k1_fn_cmp(v0, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        int x = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k1_fn_cmp(v0, pr), 64 * wv, lds) != hipSuccess) x = 0;
+        nb = std::min(nb, x);
+      }
+      if (nb * wv > bestc) {
+        bestc = nb * wv;
+        e->k1c_waves = wv;
+        e->k1c_blocks_per_cu = std::max(1, nb);
+        e->k1c_lds = lds;
+      }
+    }
+    e->k1c_wave_dbl = WL0.total;
+    for (int pr = 0; pr < 3 && st == hipSuccess; ++pr)
+      st = hipFuncSetAttribute(k1_fn_cmp(v0, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1c_lds);
+    if (bestc <= 0) {
+      set_err(nullptr, SYSID_E_MODEL, "model needs too much LDS per sample (%zu B)", (size_t)WL0.total * 8);
+      sysid_destroy(e);
+      return SYSID_E_MODEL;
+    }
   }
   if (st != hipSuccess) {
     set_err(nullptr, SYSID_E_DEVICE, "device setup failed: %s", hipGetErrorString(st));
@@ -1214,38 +1311,5 @@ int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4) {
   cfg4[3] = e->k1_maxch_tpl;
   return SYSID_OK;
 }
-
-#ifdef SYSID_STAMPS
-int32_t sysid_debug_stamps(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel,
-                           int64_t ld_panel, uint64_t* out16) {
-  HIP_TRY(e, hipSetDevice(e->device));
-  HIP_TRY(e, hipMalloc(&e->d_dump, 16 * sizeof(uint64_t)));
-  HIP_TRY(e, hipMemset(e->d_dump, 0, 16 * sizeof(uint64_t)));
-  int rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, e->d_work, e->stream, e->d_dump);
-  HIP_TRY(e, hipStreamSynchronize(e->stream));
-  HIP_TRY(e, hipMemcpy(out16, e->d_dump, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  (void)hipFree(e->d_dump);
-  e->d_dump = nullptr;
-  return rc;
-}
-#endif
-
-#ifdef SYSID_EXPERIMENTS
-// Experiments only: K2 (+K3 when final) on an existing panel, on a given stream.
-int32_t sysid_exp_k2(sysid_engine* e, const double* d_panel, int64_t N, int64_t ld_panel, int32_t accumulate,
-                     int32_t final, double* d_gram, void* d_ws, size_t ws_bytes, void* stream) {
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const int64_t rows = N * e->nv;
-  const int ks = ksplit_for(e, rows);
-  double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-  int rc = launch_k2(e, d_panel, rows, ld_panel, ks, accumulate, slab, st, 0);
-  if (rc == SYSID_OK && final) rc = launch_k3(e, ks, slab, d_gram, st);
-  return rc;
-}
-int32_t sysid_exp_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
-                     void* stream) {
-  return launch_k1(e, d_in, N, ld, d_panel, ld_panel, e->d_work, static_cast<hipStream_t>(stream), nullptr);
-}
-#endif
 
 }  // extern "C"

@@ -353,18 +353,6 @@ __device__ __forceinline__ void panel_store(__bf16* p, double a, double b) {
   *reinterpret_cast<bf16x2_t*>(p) = v;
 }
 
-#ifdef SYSID_STAMPS
-// Diagnostics build: per-phase shader-clock deltas accumulated in registers (s_memtime is uniform, so
-// every lane holds the same values) and added to dbg[0..7] once per wave at exit.
-#define K1_STAMP(k)                                                                                 \
-  {                                                                                                 \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                     \
-    t_acc[k] += _t - t_prev;                                                                        \
-    t_prev = _t;                                                                                    \
-  }
-#else
-#define K1_STAMP(k)
-#endif
 
 // Columns 0..3 (m, mc) of the block: F[6c .. 6c+5] = [linear; angular] of column c.
 __host__ __device__ inline void body_block_mass(const double* bi, double* F) {
@@ -452,22 +440,24 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 // SPW: samples per wave (1 or 2).  With SPW > 1 each 64/SPW-lane slice of the wave carries its own
 // sample through every phase, so the lane-starved serial phases (forward pass, Gram-Schmidt steps) do SPW
 // samples per instruction; each slice has its own LDS region.
-#ifndef SYSID_EXP_SKIP
-#define SYSID_EXP_SKIP 0  // diagnostics builds only: bit mask of K1 phases to skip (timing attribution)
-#endif
-template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0>
-#ifndef SYSID_K1_MIN_WAVES_PER_EU
-#define SYSID_K1_MIN_WAVES_PER_EU 1
-#endif
-#ifndef SYSID_PRIO
-#define SYSID_PRIO 1  // column phase at low issue priority, the latency-bound phases high (K1 -2%)
-#endif
+// CMP: Gram-only nullspace mode (north_star "batched QR/nullspace"): instead of P·A (nv rows
+// per sample) the sample emits Zᵀ·A, m = nv - rank(J_c) rows, with Zᵀ ((m x nv), orthonormal rows, ZᵀZ = P)
+// completed from the Gram-Schmidt basis Q by Householder reconstruction (tests/alg_mirror.py nullspace_rows):
+// Σ (ZᵀA)ᵀ(ZᵀA) = Σ AᵀPA = Σ (PA)ᵀ(PA), the same Gram from fewer rows.  Sample s keeps its rows at
+// [s·nv, s·nv + m) of the chunk panel and records m in rcount[s], from which k1s_seg_sums / k1s_row_list build
+// the list of live rows the Gram kernels gather.
+constexpr int K1_SEG_LOG = 10;  // samples per row-count segment of the CMP mode (1024)
+constexpr int K1_CMP_KMAX = 12;
+  // CMP mode: at most 12 contact rows (4 contact frames; the host checks)
+template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0>
 // Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
 // The P overlay's instantiations run 8 one-sample waves per workgroup (one 8-wave workgroup per CU).
-__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 ? 2 : SYSID_K1_MIN_WAVES_PER_EU)
+__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 ? 2 : 1)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
                    int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
-                   unsigned long long* __restrict__ work, double* __restrict__ dbg) {
+                   unsigned long long* __restrict__ work, double* __restrict__ dbg,
+                   int* __restrict__ rcount) {
+  static_assert(!(POV && CMP), "the nullspace mode runs the plain layout");
   extern __shared__ double smem[];
   const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
   {
@@ -596,14 +586,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     commit();
   }
   int64_t s1 = s < N ? claim_value(claim_issue()) : N;
-#ifdef SYSID_STAMPS
-  unsigned long long t_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
-#endif
-
-#if SYSID_PRIO
+  // issue priority: the column phase runs at 0, everything else at 2, so a wave in a latency-bound phase
+  // issues first when its operands arrive (K1 -1 to -2%, Spot and G1)
   __builtin_amdgcn_s_setprio(2);
-#endif
   const int hl_outer = hl;
   while (s < N) {
     // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
@@ -644,7 +629,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       body[x] = v;
     }
     wsync();
-    K1_STAMP(0)
 
     // ---- forward pass (computeJointTorqueRegressor forward step), in two parts ----
     // (1) here: joint placements liMi = jointPlacement * M_J(q) of every joint at once (one lane per joint:
@@ -671,7 +655,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       for (int k = 0; k < 9; ++k) bj[k] = oR[k];
       bj[9] = ot[0]; bj[10] = ot[1]; bj[11] = ot[2];
     };
-    if constexpr (!(SYSID_EXP_SKIP & 1)) {  // diagnostics builds may skip this phase (forward kinematics)
     for (int j = 1 + hl; j < NJ; j += HW) {
       double* bj = body + BODY_STRIDE * j;
       if (jtype[j] == JT_FREEFLYER) {
@@ -693,10 +676,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         if (depth[j] == lvl) pose_step(j);
       wsync();
     }
-    }
-    K1_STAMP(1)
 
-    if constexpr (!(SYSID_EXP_SKIP & 2)) {  // diagnostics builds may skip this phase (axes)
     // ---- world motion axes of every dof; contact points ----
     for (int e = hl; e < nv + nc; e += HW) {
       if (e < nv) {
@@ -731,8 +711,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         pfs[3 * c] = x[0] + bj[9]; pfs[3 * c + 1] = x[1] + bj[10]; pfs[3 * c + 2] = x[2] + bj[11];
       }
     }
-    }
-    if constexpr (!(SYSID_EXP_SKIP & 1)) {  // diagnostics builds may skip this phase (forward kinematics)
     // ---- forward pass, part (2): body velocities and accelerations ----
     // In base coordinates (the free-flyer frame) the recursion a_j = X_jp a_p + S_j ddq_j + v_j x S_j dq_j
     // reads A_j = A_p + S_d ddq_d + V_p x S_d dq_d (the adjoint commutes with the motion cross product, and
@@ -792,16 +770,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll
       for (int k = 0; k < 6; ++k) { bj[12 + k] = vb[k]; bj[18 + k] = ab[k]; }
     }
-    }
     // contacts with a non-zero value as a bit mask (independent loads, no search loop per entry below)
     unsigned long long amask = 0ull;
     for (int c = 0; c < nc; ++c) amask |= (cnt[c] != 0.0 ? 1ull : 0ull) << c;
     const int na = __popcll(amask);
     const int k = 3 * na;
     wsync();
-    K1_STAMP(2)
 
-    if constexpr (!(SYSID_EXP_SKIP & 4)) {  // diagnostics builds may skip this phase (J_c)
     // ---- contact Jacobian (LOCAL_WORLD_ALIGNED, linear rows) ----
     // lane = (contact in contact, dof): the three rows of the contact at once (one cross product)
     for (int e = hl; e < na * nv; e += HW) {
@@ -829,11 +804,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     }
     wsync();
 
-    }
     // H1 = P[:, ff] J_w[:, ff]^T is P's free-flyer columns: in base coordinates the free-flyer's motion axes
     // are the unit vectors (oR = I, ot = 0), J_w[:, ff] = I exactly.  The column phase reads those P entries
     // in place (an even ff0 keeps the rows' 16-byte alignment); otherwise H1 is copied out below.
     const bool h1_in_p = kp.has_ff && (kp.ff0 & 1) == 0;
+    int nrows = nv;  // output rows of the sample: nv, or nv - rank(J_c) in the nullspace mode (CMP)
     if (kp.full) {
       // get_full_regressor_force (src/sys_identification.py:391-399): no projection.  With the overlay P = I
       // is written after the tau column below (which reads J_c, under P's slot there).
@@ -862,7 +837,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       auto mgs_lds = [&]() {
         for (int j = hl; j < k; j += HW) nrm[j] = mgs_sqnorm<NVC>(Jc + j * nv, nv);
         wsync();
-        K1_STAMP(3)
         {
           double nmax = 0.0;
           for (int j = 0; j < k; ++j) nmax = fmax(nmax, nrm[j]);
@@ -921,7 +895,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           wsync();
         }
       };
-      if constexpr (!(SYSID_EXP_SKIP & 8)) {  // diagnostics builds may skip this phase (MGS)
       if constexpr (NVC == 18 && HW == 32) {
         if (2 * k <= HW) {
           // Quadruped form: lane pair (2j, 2j+1) keeps its half-row of row j in registers through every
@@ -943,7 +916,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           double myn = pair_sum(a0 + a1);
           if (row && h == 0) nrm[j] = myn;
           wsync();
-          K1_STAMP(3)
           double nmax = 0.0;
           for (int jj = 0; jj < k; ++jj) nmax = fmax(nmax, nrm[jj]);
           const double thr = kp.thr_rel * kp.thr_rel * nmax;
@@ -983,6 +955,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll
             for (int u = 0; u < H2; ++u)
               if (u < n2) xrow[u] = make_double2(xv[u].x * sc, xv[u].y * sc);
+            if (CMP && h == 0) nrm[j] = -sc;  // taken rows < 0, as in mgs_lds (read by the nullspace phase)
           }
           wsync();
         } else {
@@ -991,10 +964,112 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       } else {
         mgs_lds();
       }
-      }
-      K1_STAMP(4)
 
-      if constexpr (!(SYSID_EXP_SKIP & 16)) {  // diagnostics builds may skip this phase (P)
+      if constexpr (CMP) {
+        // ---- nullspace rows Zᵀ (m x nv, m = nv - r) in P's slot, row t at Ps + t nv ----
+        // (a) Householder vectors of the QR of Qᵀ (nv x r, orthonormal columns = the r taken rows of J_c, in
+        //     row order) by the unpivoted LU of Qᵀ - diag(s), s_a = -sign(d_a): every pivot d_a + sign(d_a) has
+        //     modulus >= 1, so no pivoting is needed (Householder reconstruction).  In registers: lane = column i
+        //     of Qᵀ (coordinate i), x[b] = entry i of taken row b; the pivot row's entries come by readlane.  Then
+        //     v_a (0 before a, 1 at a, x_{i,a}/piv past it: whole rows, so the products below need no masks) is
+        //     stored as J_c row a and tau_a = |d_a| + 1 = 2 / v_aᵀv_a as nrm[a].
+        unsigned long long tm = 0ull;
+        for (int j = 0; j < k; ++j) tm |= (nrm[j] < 0.0 ? 1ull : 0ull) << j;
+        const int rk = __popcll(tm);
+        {
+          double x[K1_CMP_KMAX];
+          {
+            unsigned long long rb = tm;
+#pragma unroll
+            for (int u = 0; u < K1_CMP_KMAX; ++u) {
+              const int pb = rb ? __ffsll((long long)rb) - 1 : 0;
+              rb &= rb - 1ull;
+              x[u] = u < rk && hl < nv ? Jc[pb * nv + hl] : 0.0;
+            }
+          }
+          // the value of lane `src` of this sample's lanes (two samples per wave: either half)
+          auto bcast = [&](double v, int src) -> double {
+            if constexpr (SPW == 1) return readlane_f64(v, src);
+            else return __shfl(v, half * HW + src, 64);  // each half its own source lane (ds_bpermute)
+          };
+          double tau[K1_CMP_KMAX];
+#pragma unroll
+          for (int a = 0; a < K1_CMP_KMAX; ++a) {
+            tau[a] = 0.0;
+            if (a < rk) {
+              const double d = bcast(x[a], a);
+              const double rp = 1.0 / (d + (d >= 0.0 ? 1.0 : -1.0));
+              tau[a] = fabs(d) + 1.0;
+              const double l = x[a] * rp;
+#pragma unroll
+              for (int b2 = a + 1; b2 < K1_CMP_KMAX; ++b2) {
+                const double xab = bcast(x[b2], a);
+                if (hl > a) x[b2] -= l * xab;
+              }
+              x[a] = hl > a ? l : (hl == a ? 1.0 : 0.0);
+            }
+          }
+          wsync();  // every J_c / nrm read above precedes the stores
+          if (hl < nv) {
+#pragma unroll
+            for (int a = 0; a < K1_CMP_KMAX; ++a)
+              if (a < rk) Jc[a * nv + hl] = x[a];
+          }
+          if (hl < rk) {
+#pragma unroll
+            for (int a = 0; a < K1_CMP_KMAX; ++a)
+              if (a == hl) nrm[a] = tau[a];
+          }
+          wsync();
+        }
+        // (b) row t of Zᵀ = (H_1 ... H_r e_{r+t})ᵀ, H_a = I - tau_a v_a v_aᵀ applied from a = r-1 down
+        const int m = nv - rk;
+        nrows = m;
+        if constexpr (NVC == 18 && HW == 32) {
+          if (hl < m) {  // lane = row, the row in registers
+            double y[NVC];
+#pragma unroll
+            for (int i = 0; i < NVC; ++i) y[i] = i == rk + hl ? 1.0 : 0.0;
+            for (int a = rk - 1; a >= 0; --a) {
+              const double2* qa = reinterpret_cast<const double2*>(Jc + a * NVC);
+              // v_a read twice from LDS (a register copy of it spilled): dot product, then the update
+              double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+              for (int u = 0; u < NVC / 2; ++u) {
+                const double2 x = qa[u];
+                d0 += x.x * y[2 * u];
+                d1 += x.y * y[2 * u + 1];
+              }
+              const double c = nrm[a] * (d0 + d1);
+#pragma unroll
+              for (int u = 0; u < NVC / 2; ++u) {
+                const double2 x = qa[u];
+                y[2 * u] -= c * x.x;
+                y[2 * u + 1] -= c * x.y;
+              }
+            }
+            double2* zr = reinterpret_cast<double2*>(Ps + hl * NVC);
+#pragma unroll
+            for (int u = 0; u < NVC / 2; ++u) zr[u] = make_double2(y[2 * u], y[2 * u + 1]);
+          }
+        } else {
+          // lpr lanes per row (entries i = h mod lpr), the row in place at its output position
+          const int lpr = 2 * m <= HW ? 2 : 1;
+          for (int it = hl; it < m * lpr; it += HW) {
+            const int t = it / lpr, h = it - t * lpr;
+            double* y = Ps + t * nv;
+            for (int i = h; i < nv; i += lpr) y[i] = i == rk + t ? 1.0 : 0.0;
+            for (int a = rk - 1; a >= 0; --a) {
+              const double* qa = Jc + a * nv;  // the whole v_a (zeros before a)
+              double dot = 0.0;
+              for (int i = h; i < nv; i += lpr) dot += qa[i] * y[i];
+              const double c = nrm[a] * group_sum(dot, lpr);
+              for (int i = h; i < nv; i += lpr) y[i] -= c * qa[i];
+            }
+          }
+        }
+        wsync();
+      } else {
       // ---- P = I - Q^T Q  (Zt row a = column a of Q; J_c rows = rows of Q) ----
       if constexpr (NVC == 18 && HW == 32) {
         // Register-blocked: lane = (row pair, 6-column group), 27 lanes x 12 entries, every load before
@@ -1077,12 +1152,10 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       }
     }
-    K1_STAMP(5)
 
-    if constexpr (!(SYSID_EXP_SKIP & 32)) {  // diagnostics builds may skip this phase (tp/H1)
     // ---- tp = P S^T tau  (+ J_c^T lambda in the full mode) ;  H1 = P[:, ff] J_w[:, ff]^T ----
     // tp first: in the full mode H1 may be stored over J_c (overlay layout), which the tau column reads.
-    for (int r = hl; r < nv; r += HW) {
+    for (int r = hl; r < nrows; r += HW) {
       double acc = 0.0;
       if (POV && kp.full) {
         acc = r >= bd && r < bd + nja ? tau[r - bd] : 0.0;  // P = I (not yet written)
@@ -1124,16 +1197,15 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       wsync();
     }
-    for (int e = hl; e < nv * 6 && !h1_in_p; e += HW) {
+    for (int e = hl; e < nrows * 6 && !h1_in_p; e += HW) {
       const int r = e / 6, c = e - 6 * r;
       H1[e] = kp.has_ff ? Ps[r * nv + kp.ff0 + c] : 0.0;  // J_w[:, ff] = I (see h1_in_p)
     }
     wsync();
-    }
-    if (dbg != nullptr && s + half == 0) {
-#ifndef SYSID_STAMPS
-      for (int x = hl; x < L.total; x += HW) dbg[x] = wr[x];  // diagnostics: LDS image of sample 0
-#endif
+    if (dbg != nullptr && s + half == 0)  // sysid_debug_lds: the LDS image of sample 0
+      for (int x = hl; x < L.total; x += HW) dbg[x] = wr[x];
+    if constexpr (CMP) {
+      if (hl == 0 && valid) rcount[s + half] = nrows;
     }
     // mid-step: the next inputs go to `in` (the friction columns keep this sample's dq in dqs)
     for (int x = hl; x < nv; x += HW) dqs[x] = dq[x];
@@ -1143,11 +1215,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     if (s1 < N) commit();
     wsync();
-    K1_STAMP(6)
 
-#if SYSID_PRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
@@ -1196,26 +1265,20 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       for (int t = 0; t < MAXCH; ++t) dof[t] = t < cl ? chain[i * kp.maxch + t] : 0;
       return cl;
     };
-#ifndef SYSID_STAGE_Y
-#define SYSID_STAGE_Y 1
-#endif
     // Quadrupeds: the rg = 2 row groups' current rows are staged in LDS over the joint records (dead
     // once every lane holds its block F) and written out as whole contiguous panel rows: one 16-byte
     // store per lane per 512 contiguous bytes instead of 16-byte pieces 80 bytes apart.
     // (The host picks this kernel only for 11..16 bodies: rg = 2 row groups, nyi <= 32 lanes, and the two
-    // staged rows fit in the joint records.)
-#ifndef SYSID_K1_COLV
-#define SYSID_K1_COLV 2
-#endif
-    if constexpr (!(SYSID_EXP_SKIP & 64)) {  // diagnostics builds may skip this phase (Y_proj columns)
-    if constexpr (SYSID_STAGE_Y && NVC == 18 && HW == 32) {
-      constexpr int RH = NVC / 2;  // rows per row group
+    // staged rows fit in the joint records.)  Group g takes rows [g rh, g rh + rh) of the sample's nrows.
+    if constexpr (NVC == 18 && HW == 32) {
+      // rows per row group; the nullspace mode rounds it to even (row pairs, no odd tail: fewer registers) and
+      // skips the stores of rows >= nrows
+      const int rh = CMP ? ((nrows + 3) >> 2) << 1 : NVC / 2;
       const bool act = hl < nyi && valid;
       const int g = hl / nbody, i = hl - g * nbody + 1;  // lanes past nyi compute a real body's block
       double F[FBLK];
       int dof[MAXCH];
       const int cl = block_setup(i, F, dof);
-#if SYSID_K1_COLV >= 2
       // The chain's motion axes are the same for every row: read once into registers (masked past the
       // chain), and each row's H1 / P entries are loaded one row ahead, so a row's LDS reads are in flight
       // while the previous row is multiplied and staged.
@@ -1225,7 +1288,8 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll
         for (int k = 0; k < 6; ++k) jw[t][k] = t < cl ? Jws[6 * dof[t] + k] : 0.0;
       double hn[6], pn[MAXCH];
-      auto row_load = [&](int r, double* h, double* pp) {
+      auto row_load = [&](int r, double* h, double* pp) {  // rows >= nrows: unused values from P's slot
+        if constexpr (CMP) r = r < NVC ? r : NVC - 1;
         const double2* h2 = reinterpret_cast<const double2*>(h1_in_p ? Ps + r * NVC + kp.ff0 : H1 + 6 * r);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -1236,22 +1300,17 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 #pragma unroll
         for (int t = 0; t < MAXCH; ++t) pp[t] = Ps[r * NVC + dof[t]];
       };
-      row_load(g * RH, hn, pn);
-#endif
+      row_load(g * rh, hn, pn);
       wsync();  // every read of the joint records precedes the first staging store
       double* stg = body;  // [row group][wy]
       const int wy2 = kp.wy >> 1, n2 = kp.rg * wy2;
-#ifndef SYSID_K1_YST_SBASE
-#define SYSID_K1_YST_SBASE 1
-#endif
-#ifndef SYSID_K1_YPP
-#define SYSID_K1_YPP 1
-#endif
-#if SYSID_K1_YST_SBASE
+      // pair x of row group gg lands at row gg*rh + rho, column 2*(x - gg*wy2): from this row's start that is
+      // 2x, plus dg for the second group.  The row start of the wave's first sample is wave-uniform (scalar
+      // registers); the second sample's rows and the column go into a 32-bit lane byte offset, so each store is
+      // a scalar-base + lane-offset store with no 64-bit address math.
       char* ybase = reinterpret_cast<char*>(panel + (s * NVC) * ldp);
       const uint32_t yhoff = (uint32_t)(half * NVC * (int)ldp * (int)sizeof(OutT));
-#endif
-#if SYSID_K1_YPP && SYSID_K1_COLV >= 2 && !defined(SYSID_EXP_NO_YCOMP)
+      const int dg = rh * (int)ldp - kp.wy;
       // Rows in pairs with two explicit H1 / P register sets (no copies between them): row rho + 1's LDS reads
       // are in flight while row rho is multiplied, staged and stored.  The P entries past the body's chain
       // (dof slot 0, a finite entry of P) meet zero motion axes (jw), so they add exact zeros: no mask.
@@ -1279,92 +1338,39 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         wsync();
         if (valid) {
           const double2* s2 = reinterpret_cast<const double2*>(stg);
-          const int dg = RH * (int)ldp - kp.wy;
           char* rb = ybase + (int64_t)rho * ldp * (int64_t)sizeof(OutT);
-          for (int x = hl; x < n2; x += HW) {
+          // nullspace mode: the rows past nrows of either group are not stored
+          const int n2v = !CMP ? n2 : rh + rho < nrows ? n2 : rho < nrows ? wy2 : 0;
+          for (int x = hl; x < n2v; x += HW) {
             const uint32_t off = yhoff + (uint32_t)((2 * x + (x >= wy2 ? dg : 0)) * (int)sizeof(OutT));
             panel_store(reinterpret_cast<OutT*>(rb + off), s2[x].x, s2[x].y);
           }
         }
         wsync();
       };
-      int rho = 0;
+      if constexpr (CMP) {
 #pragma unroll 1
-      for (; rho + 1 < RH; rho += 2) {
-        row_load(g * RH + rho + 1, hB, pB);
-        yrow(rho, hn, pn);
-        if (rho + 2 < RH) row_load(g * RH + rho + 2, hn, pn);
-        yrow(rho + 1, hB, pB);
-      }
-      if (rho < RH) yrow(rho, hn, pn);
-#else
+        for (int rho = 0; rho < rh; rho += 2) {
+          row_load(g * rh + rho + 1, hB, pB);
+          yrow(rho, hn, pn);
+          row_load(g * rh + rho + 2, hn, pn);
+          yrow(rho + 1, hB, pB);
+        }
+      } else {
+        int rho = 0;
 #pragma unroll 1
-      for (int rho = 0; rho < RH; ++rho) {
-        if (act) {
-          double y[10];
-#if defined(SYSID_EXP_NO_YCOMP)
-#pragma unroll
-          for (int c = 0; c < 10; ++c) y[c] = F[c];  // diagnostics build: no row products
-#elif SYSID_K1_COLV >= 2
-          double G[6], pc[MAXCH];
-#pragma unroll
-          for (int k = 0; k < 6; ++k) G[k] = hn[k];
-#pragma unroll
-          for (int t = 0; t < MAXCH; ++t) pc[t] = pn[t];
-          if (rho + 1 < RH) row_load(g * RH + rho + 1, hn, pn);
-#pragma unroll
-          for (int t = 0; t < MAXCH; ++t) {
-            const double pv = t < cl ? pc[t] : 0.0;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) G[k] += pv * jw[t][k];
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            y[c] = G[0] * F[6 * c] + G[1] * F[6 * c + 1] + G[2] * F[6 * c + 2] + G[3] * F[6 * c + 3] +
-                   G[4] * F[6 * c + 4] + G[5] * F[6 * c + 5];
-#pragma unroll
-          for (int c = 0; c < 6; ++c)
-            y[4 + c] = G[3] * F[24 + 3 * c] + G[4] * F[24 + 3 * c + 1] + G[5] * F[24 + 3 * c + 2];
-#else
-          block_row(g * RH + rho, F, dof, cl, y);
-#endif
-          double2* sp = reinterpret_cast<double2*>(stg + g * kp.wy + 10 * (i - 1));
-#pragma unroll
-          for (int c = 0; c < 5; ++c) sp[c] = make_double2(y[2 * c], y[2 * c + 1]);
+        for (; rho + 1 < rh; rho += 2) {
+          row_load(g * rh + rho + 1, hB, pB);
+          yrow(rho, hn, pn);
+          if (rho + 2 < rh) row_load(g * rh + rho + 2, hn, pn);
+          yrow(rho + 1, hB, pB);
         }
-        wsync();
-        if (valid) {
-          const double2* s2 = reinterpret_cast<const double2*>(stg);
-          // pair x of row group gg lands at row gg*RH + rho, column 2*(x - gg*wy2): from this row's start
-          // that is 2x, plus dg for the second group.  The row start of the wave's first sample is
-          // wave-uniform (scalar registers); the second sample's rows and the column go into a 32-bit lane
-          // byte offset, so each store is a scalar-base + lane-offset store with no 64-bit address math.
-          const int dg = RH * (int)ldp - kp.wy;
-#if SYSID_K1_YST_SBASE
-          char* rb = ybase + (int64_t)rho * ldp * (int64_t)sizeof(OutT);
-#else
-          OutT* orow = out + (int64_t)rho * ldp;
-#endif
-          for (int x = hl; x < n2; x += HW) {
-#ifndef SYSID_EXP_NO_YSTORE
-#if SYSID_K1_YST_SBASE
-            const uint32_t off = yhoff + (uint32_t)((2 * x + (x >= wy2 ? dg : 0)) * (int)sizeof(OutT));
-            panel_store(reinterpret_cast<OutT*>(rb + off), s2[x].x, s2[x].y);
-#else
-            panel_store(orow + 2 * x + (x >= wy2 ? dg : 0), s2[x].x, s2[x].y);
-#endif
-#else
-            if (s2[x].x == 1.2345e300) panel_store(out, s2[x].x, s2[x].y);  // diagnostics build: keep the reads
-#endif
-          }
-        }
-        wsync();
+        if (rho < rh) yrow(rho, hn, pn);
       }
-#endif
     } else {
       for (int it = hl; it < nyi && valid; it += HW) {
         const int g = it / nbody, i = it - g * nbody + 1;
-        const int r0 = g * nv / kp.rg, r1 = (g + 1) * nv / kp.rg;
+        const int r0 = g * nrows / kp.rg, r1 = (g + 1) * nrows / kp.rg;
         double F[FBLK];
         int dof[MAXCH];  // the chain's dofs, read once: no dependent index load per row
         const int cl = block_setup(i, F, dof);
@@ -1378,10 +1384,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
       }
     }
-
-    }
-    K1_STAMP(8)
-    if constexpr (!(SYSID_EXP_SKIP & 128)) {  // diagnostics builds may skip this phase (friction/torque columns)
     // ---- [B_v | B_c | tau_proj | pad]: 16-byte stores of column pairs ----
     // Up to 32 pairs (nj <= 31): lane = column pair m within a group of gs = 8, 16 or 32 lanes (the
     // narrowest that holds the pairs), the HW/gs groups taking every (HW/gs)-th row, so a lane's dq / sign(dq)
@@ -1409,21 +1411,17 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
         OutT* po = out + (int64_t)fg * ldp + kp.wy + 2 * m;  // advanced by NG rows per pass
         const int64_t pstep = (int64_t)NG * ldp;
-        for (int r = fg; r < nv; r += NG, po += pstep) {
+        for (int r = fg; r < nrows; r += NG, po += pstep) {
           const double* pr = Ps + r * nv + bd;
           const double t = tps[r];
           double v2[2];
 #pragma unroll
           for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pr[jc[u]] * sc[u] : (tcol[u] ? t : 0.0);  // pad: whole lines
-#ifndef SYSID_EXP_NO_FSTORE
           panel_store(po, v2[0], v2[1]);
-#else
-          if (v2[0] == 1.2345e300) panel_store(out, v2[0], v2[1]);  // diagnostics build
-#endif
         }
       }
     } else {
-      for (int it = hl; it < nv * npair && valid; it += HW) {
+      for (int it = hl; it < nrows * npair && valid; it += HW) {
         const int r = it / npair, m = it - r * npair;
         const double* pr = Ps + r * nv + bd;
         double v2[2];
@@ -1438,25 +1436,77 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           const double fr = pr[jc] * sc;
           v2[u] = jj < 2 * nja ? fr : (kp.wy + jj == kp.w ? tps[r] : 0.0);  // pad: keep lines whole
         }
-#ifndef SYSID_EXP_NO_FSTORE
         panel_store(out + (int64_t)r * ldp + kp.wy + 2 * m, v2[0], v2[1]);
-#else
-        if (v2[0] == 1.2345e300) panel_store(out, v2[0], v2[1]);  // diagnostics build
-#endif
       }
     }
-    }
-#if SYSID_PRIO
     __builtin_amdgcn_s_setprio(2);
-#endif
-    K1_STAMP(7)
     s = s1;
     s1 = s2;
   }
-#ifdef SYSID_STAMPS
-  if (lane == 0)
-    for (int k = 0; k < 9; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + k, t_acc[k]);
-#endif
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1s (nullspace mode): the list of live chunk-panel rows, in sample order, for the Gram kernels to gather.
+// k1s_seg_sums: rseg[b] = the rows of the 1024 samples of segment b.  k1s_row_list: block b's first list
+// position is the sum of the earlier segments' rows, then a block scan of its own samples' counts; sample s
+// with m rows lists s·nv, ..., s·nv + m - 1.  The last block writes the total.  Plain stores and integer
+// arithmetic only (no atomics, nothing to zero beforehand): deterministic, and graph replays start clean.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int k1s_wave_incl(int v, int lane) {  // inclusive scan over the 64 lanes
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(256)
+k1s_seg_sums(const int* __restrict__ rcount, int n, int* __restrict__ rseg) {
+  __shared__ int wsum[4];
+  const int b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+  const int s0 = (b << K1_SEG_LOG) + 4 * t;
+  int loc = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) loc += s0 + u < n ? rcount[s0 + u] : 0;
+  loc = __shfl(k1s_wave_incl(loc, lane), 63, 64);
+  if (lane == 0) wsum[w] = loc;
+  __syncthreads();
+  if (t == 0) rseg[b] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ void __launch_bounds__(256)
+k1s_row_list(const int* __restrict__ rcount, const int* __restrict__ rseg, int n, int nv, int* __restrict__ rowlist,
+             int* __restrict__ total) {
+  __shared__ int wsum[4];
+  const int b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+  auto wave_incl = [&](int v) { return k1s_wave_incl(v, lane); };
+  int pre = 0;
+  for (int x = t; x < b; x += 256) pre += rseg[x];
+  pre = __shfl(wave_incl(pre), 63, 64);
+  if (lane == 0) wsum[w] = pre;
+  __syncthreads();
+  const int base = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  int c[4], loc = 0;
+  const int s0 = (b << K1_SEG_LOG) + 4 * t;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    c[u] = s0 + u < n ? rcount[s0 + u] : 0;
+    loc += c[u];
+  }
+  const int incl = wave_incl(loc);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int o = base + incl - loc;
+  for (int x = 0; x < w; ++x) o += wsum[x];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r0 = (s0 + u) * nv;
+    for (int j = 0; j < c[u]; ++j) rowlist[o + j] = r0 + j;
+    o += c[u];
+  }
+  if (b == (int)gridDim.x - 1 && t == 255) *total = o;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1483,39 +1533,20 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __host__ __device__ constexpr int k2_waves(int ntc) { return ntc < 16 ? 16 : 8; }
 __host__ __device__ constexpr int k2_spw(int ntc) { return ntc < 16 ? 1 : 2; }
 constexpr int K2_BF16_WAVES = 8;  // the bf16 kernel's waves
-// Super-tile slots per wave of the bf16 kernel.  A bf16 k-step is only 16 MFMA cycles per tile, so the kernel
-// is fed, not MFMA, bound: every super-tile group re-reads (and re-stages) the whole panel, and with the f64
-// kernels' 16 slots per group G1 (78 super-tiles) took 5 groups = 5 panel reads (G1 125k K2 3.1 ms, ~5 TB/s of
-// staged rows, the same with XCD-local groups).  Wide Grams take 5 slots per wave here (40 per group: G1 in
-// 2 groups; 80 f32 accumulator VGPRs, fragments loaded per slot); the bf16 kernel has its own super-tile deal.
-// Super-tile slots per wave of the f64 / f32 kernels.  Wide f32 Grams take more (f32 accumulators are half
-// the f64 registers), so fewer groups re-read the panel (see k2_bf16_spw below).
-#ifndef SYSID_K2_F32_SPW
-#define SYSID_K2_F32_SPW 2
-#endif
+// Super-tile slots per wave of the f64 / f32 kernels (f32 keeps 2 for wide Grams: 4 measured 1.5% faster,
+// 5 cost a workgroup per CU, profiles/r02_ab3/k2_f32_slots_per_wave_g1_125k.txt).
 template <typename T>
-__host__ __device__ constexpr int k2_slots(int ntc) {
-  return sizeof(T) == 4 && ntc >= 16 ? SYSID_K2_F32_SPW : k2_spw(ntc);
-}
-#ifndef SYSID_K2_BF16_SPW
-#define SYSID_K2_BF16_SPW 5
-#endif
-#ifndef SYSID_K2_BF16_TR
-#define SYSID_K2_BF16_TR 1  // wide Grams on k2_gram_syrk_bf16_tr (LDS-DMA + transposed fragment reads)
-#endif
-#ifndef SYSID_K2_BF16_TR_SPW
-#define SYSID_K2_BF16_TR_SPW 10
-#endif
+__host__ __device__ constexpr int k2_slots(int ntc) { return k2_spw(ntc); }
+// Super-tile slots per wave of the bf16 kernels.  A bf16 k-step is only 16 MFMA cycles per tile, so the kernel
+// is fed, not MFMA, bound: every super-tile group re-reads (and re-stages) the whole panel, and with the f64
+// kernels' 16 slots per group G1 (78 super-tiles) took 5 groups = 5 panel reads (G1 125k K2 3.1 ms).  Wide
+// Grams run k2_gram_syrk_bf16_tr with 10 slots per wave (all of G1's super-tiles in one workgroup: the panel is
+// read once; 5 slots: 1.64 vs 1.49 ms); narrow ones the f64 kernels' deal.
 __host__ __device__ constexpr int k2_bf16_spw(int ntc) {
-  return ntc >= 16 ? (SYSID_K2_BF16_TR ? SYSID_K2_BF16_TR_SPW : SYSID_K2_BF16_SPW)
-                   : k2_waves(ntc) * k2_spw(ntc) / K2_BF16_WAVES;
+  return ntc >= 16 ? 10 : k2_waves(ntc) * k2_spw(ntc) / K2_BF16_WAVES;
 }
-#ifndef SYSID_K2_UNIFORM
-#define SYSID_K2_UNIFORM 0  // readfirstlane'd descriptors measured slower (G1 K2 1.80 -> 2.26 ms, Spot +3%)
-#endif
-#ifndef SYSID_K2_ALLTILES
-#define SYSID_K2_ALLTILES 0  // computing the redundant tiles too measured slower (Spot +6%, G1 +9%)
-#endif
+// Measured and not kept: readfirstlane'd descriptors in the f64 kernels (G1 K2 1.80 -> 2.26 ms, Spot +3%);
+// computing the redundant lower tiles of diagonal super-tiles too (Spot +6%, G1 +9%).
 
 // Reduced-precision Gram (error reported, not gated): T = float runs the same
 // kernel on v_mfma_f32_16x16x4_f32 (panel rounded to f32 while staged, f32 accumulation per workgroup,
@@ -1535,12 +1566,9 @@ __device__ __forceinline__ bool k2_tile_skip(int2 sp, int t) { return sp.x >= 0 
 // (G1 K2 at ~6 TB/s of re-reads).  Here the blocks of one XCD take consecutive (ks, group) pairs, so a
 // slice's groups share an L2 and run side by side: one HBM read, the others L2 hits.  A bijection for any
 // grid; speed only (any placement is correct).
-#ifndef SYSID_K2_XCD_MAP
-#define SYSID_K2_XCD_MAP 1
-#endif
 __device__ __forceinline__ void k2_block_coords(int ngroups, int& group, int& ks) {
   int L = (int)blockIdx.x;
-  if (SYSID_K2_XCD_MAP && ngroups > 1) {
+  if (ngroups > 1) {
     const int nb = (int)gridDim.x, x = L & 7, i = L >> 3;
     const int q = nb >> 3, r = nb & 7;  // XCD y holds q + (y < r) blocks
     L = x * q + (x < r ? x : r) + i;
@@ -1605,11 +1633,7 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int x = threadIdx.x + u * NT;
-#ifndef SYSID_EXP_K2_NOLOAD
       st[u] = (used[u] && x < lim) ? src[x] : make_uint4(0u, 0u, 0u, 0u);
-#else
-      st[u] = make_uint4((unsigned)x, 1u, 2u, 3u);  // diagnostics build: no global loads
-#endif
     }
   };
   auto store_chunk = [&](T* b) {
@@ -1625,12 +1649,6 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
   for (int s = 0; s < K2S; ++s) {
     int2 sp = supers[sbase + s];
-#if SYSID_K2_UNIFORM
-    // wave-uniform by construction (sbase depends on the wave only): SGPRs, so the tile tests below are
-    // scalar branches instead of exec-masked blocks around every MFMA
-    sp.x = __builtin_amdgcn_readfirstlane(sp.x);
-    sp.y = __builtin_amdgcn_readfirstlane(sp.y);
-#endif
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1667,11 +1685,7 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
         constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-#if SYSID_K2_ALLTILES
-          if (!live[s]) continue;  // every tile of a live super-tile: the redundant ones land in unused slots
-#else
           if (!need[s][t]) continue;
-#endif
           if constexpr (sizeof(T) == 8)
             acc[s][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
           else
@@ -1780,17 +1794,15 @@ __device__ __forceinline__ void k2_barrier() {
 
 // Rows per chunk of the DMA kernel: three buffers of KC x k2_stride(NTC) elements in the CU's 160 KB (one
 // workgroup per CU, NTC < 16) or in half of it (two, NTC >= 16); a multiple of 8 (rows are dealt to the 8 waves).
-#ifndef SYSID_K2_DMA_NARROW
-#define SYSID_K2_DMA_NARROW 0
-#endif
-__host__ __device__ constexpr int k2_dma_kc(int ntc) {
-  return ntc <= 10 ? (SYSID_K2_DMA_NARROW ? 16 : 32) : ntc < 16 ? 24 : 8;
-}
+__host__ __device__ constexpr int k2_dma_kc(int ntc) { return ntc <= 10 ? 32 : ntc < 16 ? 16 : 8; }
 
-template <typename T, int NTC, int KC>
+// GATHER (nullspace mode): the rows are those listed in rowlist (k1s_row_list), *d_rows of them; every wave
+// reads its rows' list entries for the chunk after next by scalar loads, one chunk ahead of their DMA.
+template <typename T, int NTC, int KC, bool GATHER = false>
 __global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
-                 int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+                 int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab,
+                 const int* __restrict__ rowlist, const int* __restrict__ d_rows) {
   typedef typename K2Acc<T>::type accT;
   constexpr int K2W = k2_waves(NTC), K2S = k2_slots<T>(NTC);
   static_assert(KC % K2W == 0 && KC % 4 == 0, "chunk rows are dealt to the waves, k-steps of 4");
@@ -1803,11 +1815,16 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   __shared__ __attribute__((aligned(16))) T lds[3 * BUF];
   int group, ks;
   k2_block_coords(ngroups, group, ks);
+  const int64_t prows = rows;  // GATHER: the panel's rows (the list holds at most these)
+  if constexpr (GATHER) rows = min((int64_t)__builtin_amdgcn_readfirstlane(*d_rows), prows);
   const int64_t q4 = rows / 4;
   const int64_t r0 = 4 * (q4 * ks / ksplit);
   const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sbase = (group * K2W + wave) * K2S;
+  // the wave index in a scalar register for the row list's scalar loads; the super-tile descriptors stay per
+  // lane (uniform ones measured slower, see above)
+  const int wave = GATHER ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int sbase = (group * K2W + (int)(threadIdx.x >> 6)) * K2S;
 
   // zero the three buffers once: columns >= ldp (up to NTC*16) are never written by the DMA and must read as 0
   for (int x = threadIdx.x; x < 3 * BUF; x += NT) lds[x] = (T)0;
@@ -1828,11 +1845,23 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
       }
     }
   };
+  // GATHER: the list entries of the wave's rows of the next chunk to DMA, loaded one chunk ahead (SGPRs)
+  int gidx[RPW];
+  auto list_load = [&](int64_t c0) {
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int64_t x = c0 + wave + K2W * q;
+        const int v = x < r1 ? rowlist[x] : 0;
+        gidx[q] = v >= 0 && v < prows ? v : 0;
+      }
+    }
+  };
   auto dma_chunk = [&](int64_t c0, T* buf) {  // RPW * np instructions per wave
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int rr = wave + K2W * q;
-      dma_row(panel + (c0 + rr) * ldp, buf + rr * STRIDE);
+      dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, buf + rr * STRIDE);
     }
   };
 
@@ -1886,9 +1915,12 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   T* b0 = lds;                            // chunk c
   T* b1 = lds + BUF;                      // chunk c + 1
   T* b2 = lds + 2 * BUF;                  // chunk c + 2
+  list_load(r0);
   if (nfull > 0) dma_chunk(r0, b0);
+  list_load(r0 + KC);
   if (nfull > 1) {
     dma_chunk(r0 + KC, b1);
+    list_load(r0 + 2 * KC);
     k2_wait_chunk<RPW>(np);  // chunk 0 landed (chunk 1 in flight)
   } else {
     k2_wait_vm<0>();
@@ -1896,7 +1928,10 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   k2_barrier();
   for (int64_t c = 0; c < nfull; ++c) {
     const bool pre = c + 2 < nfull;
-    if (pre) dma_chunk(r0 + (c + 2) * KC, b2);
+    if (pre) {
+      dma_chunk(r0 + (c + 2) * KC, b2);
+      list_load(r0 + (c + 3) * KC);
+    }
     mfma_chunk(b0);
     if (pre) k2_wait_chunk<RPW>(np);  // chunk c + 1 landed, chunk c + 2 stays in flight
     else k2_wait_vm<0>();
@@ -1909,12 +1944,13 @@ k2_gram_syrk_dma(const T* __restrict__ panel, int64_t rows, int64_t ldp, const i
   if (r0 + nfull * KC < r1) {  // the partial last chunk, into b0 (free: its last chunk finished two barriers ago)
     const int64_t c0 = r0 + nfull * KC;
     const int valid = (int)(r1 - c0);
+    list_load(c0);
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int rr = wave + K2W * q;
       T* dst = b0 + rr * STRIDE;
       if (rr < valid) {
-        dma_row(panel + (c0 + rr) * ldp, dst);
+        dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, dst);
       } else {
         for (int x = 16 * lane; x < rowbytes; x += 16 * 64) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst) + x) = make_uint4(0u, 0u, 0u, 0u);
       }
@@ -2032,12 +2068,6 @@ k2_gram_syrk_bf16(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, c
 #pragma unroll
   for (int s = 0; s < K2S; ++s) {
     int2 sp = supers[sbase + s];
-#if SYSID_K2_UNIFORM
-    // wave-uniform by construction (sbase depends on the wave only): SGPRs, so the tile tests below are
-    // scalar branches instead of exec-masked blocks around every MFMA
-    sp.x = __builtin_amdgcn_readfirstlane(sp.x);
-    sp.y = __builtin_amdgcn_readfirstlane(sp.y);
-#endif
     live[s] = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -2120,10 +2150,11 @@ __host__ __device__ constexpr int k2_bf16_tr_kc(int ntc) {
   return (160 * 1024 / (3 * (ntc * 16 + 8) * 2)) / 32 * 32 > 128 ? 128 : (160 * 1024 / (3 * (ntc * 16 + 8) * 2)) / 32 * 32;
 }
 
-template <int NTC, int KC>
+template <int NTC, int KC, bool GATHER = false>
 __global__ void __launch_bounds__(64 * K2_BF16_WAVES)
 k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
-                     int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+                     int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab,
+                     const int* __restrict__ rowlist, const int* __restrict__ d_rows) {
   static_assert(KC % 32 == 0 && KC % K2_BF16_WAVES == 0, "whole 32-row k-steps, rows dealt to the waves");
   constexpr int K2W = K2_BF16_WAVES, K2S = k2_bf16_spw(NTC);
   constexpr int STRIDE = NTC * 16 + 8;  // elements per LDS row (16-byte multiple)
@@ -2134,10 +2165,12 @@ k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp
   __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
   int group, ks;
   k2_block_coords(ngroups, group, ks);
+  const int64_t prows = rows;  // GATHER: the panel's rows (the list holds at most these)
+  if constexpr (GATHER) rows = min((int64_t)__builtin_amdgcn_readfirstlane(*d_rows), prows);
   const int64_t q4 = rows / 4;
   const int64_t r0 = 4 * (q4 * ks / ksplit);
   const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int sbase = (group * K2W + wave) * K2S;
 
   for (int x = threadIdx.x; x < 3 * BUF; x += NT) lds[x] = (__bf16)0.0f;  // columns >= ldp read as 0
@@ -2149,11 +2182,22 @@ k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(reinterpret_cast<const char*>(src_row) + off),
                                        reinterpret_cast<void*>(dst_row), 16, 0, 0);
   };
+  int gidx[RPW];  // GATHER: list entries of the wave's rows of the next chunk to DMA (as k2_gram_syrk_dma)
+  auto list_load = [&](int64_t c0) {
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int64_t x = c0 + wave + K2W * q;
+        const int v = x < r1 ? rowlist[x] : 0;
+        gidx[q] = v >= 0 && v < prows ? v : 0;
+      }
+    }
+  };
   auto dma_chunk = [&](int64_t c0, __bf16* buf) {  // RPW instructions per wave
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int rr = wave + K2W * q;
-      dma_row(panel + (c0 + rr) * ldp, buf + rr * STRIDE);
+      dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, buf + rr * STRIDE);
     }
   };
 
@@ -2209,9 +2253,12 @@ k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp
   __bf16* b0 = lds;
   __bf16* b1 = lds + BUF;
   __bf16* b2 = lds + 2 * BUF;
+  list_load(r0);
   if (nfull > 0) dma_chunk(r0, b0);
+  list_load(r0 + KC);
   if (nfull > 1) {
     dma_chunk(r0 + KC, b1);
+    list_load(r0 + 2 * KC);
     k2_wait_vm<RPW>();  // chunk 0 landed (chunk 1 in flight)
   } else {
     k2_wait_vm<0>();
@@ -2219,7 +2266,10 @@ k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp
   k2_barrier();
   for (int64_t c = 0; c < nfull; ++c) {
     const bool pre = c + 2 < nfull;
-    if (pre) dma_chunk(r0 + (c + 2) * KC, b2);
+    if (pre) {
+      dma_chunk(r0 + (c + 2) * KC, b2);
+      list_load(r0 + (c + 3) * KC);
+    }
     mfma_chunk(b0);
     if (pre) k2_wait_vm<RPW>();  // chunk c + 1 landed, chunk c + 2 stays in flight
     else k2_wait_vm<0>();
@@ -2232,12 +2282,13 @@ k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp
   if (r0 + nfull * KC < r1) {  // the partial last chunk into b0 (its last reads retired at the barrier above)
     const int64_t c0 = r0 + nfull * KC;
     const int valid = (int)(r1 - c0);
+    list_load(c0);
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int rr = wave + K2W * q;
       __bf16* dst = b0 + rr * STRIDE;
       if (rr < valid) {
-        dma_row(panel + (c0 + rr) * ldp, dst);
+        dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, dst);
       } else {
         for (int x = 16 * lane; x < rowbytes; x += 16 * 64)
           *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst) + x) = make_uint4(0u, 0u, 0u, 0u);

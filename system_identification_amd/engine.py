@@ -26,6 +26,9 @@ EMIT_FRICTION = 4
 EMIT_GRAM = 8
 EMIT_ALL = 15
 GRAM_F32, GRAM_BF16 = 16, 32
+GRAM_PROJECTOR = 64   # Gram-only from the reference's P·A rows (nv per sample)
+GRAM_NULLSPACE = 128  # Gram-only from the nullspace rows Zᵀ·A (nv - rank(J_c) per sample)
+GRAM_ROWS = {"auto": 0, "projector": GRAM_PROJECTOR, "nullspace": GRAM_NULLSPACE}
 GRAM_PRECISION = {"f64": 0, "f32": GRAM_F32, "bf16": GRAM_BF16}
 
 LIB_NAME = "libsysid.so"
@@ -345,9 +348,12 @@ class Engine:
             "ws": torch.empty(max(self.gram_workspace_bytes(N), 256), dtype=torch.uint8, device=dev),
         }
 
-    def build_gram_device(self, d_in, N: int, bufs: dict, stream=None, precision: str = "f64"):
+    def build_gram_device(self, d_in, N: int, bufs: dict, stream=None, precision: str = "f64",
+                          rows: str = "auto"):
         """Normal equations of N samples without materialising the N·nv-row panel (stream-ordered).
-        precision: "f64" (parity), "f32" or "bf16" (MFMA in reduced precision, error reported)."""
+        precision: "f64" (parity), "f32" or "bf16" (MFMA in reduced precision, error reported).
+        rows: "nullspace" (each sample's nv - rank(J_c) rows Zᵀ·A, ZᵀZ = P), "projector" (the reference's nv
+        rows P·A) or "auto" (nullspace for f64 / f32, projector for bf16); all give Σ AᵀPA."""
         import torch
         self._check_inputs(d_in, N)
         self._check_buffer(bufs["gram"], "gram", torch.float64, self.panel_cols * self.panel_cols)
@@ -356,7 +362,8 @@ class Engine:
         self._check_buffer(bufs["ws"], "ws", torch.uint8, self.gram_workspace_bytes(N))
         st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.sysid_build_gram_device(
-            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)), GRAM_PRECISION[precision],
+            self._h, ctypes.c_void_p(d_in.data_ptr()), int(N), int(d_in.stride(0)),
+            GRAM_PRECISION[precision] | GRAM_ROWS[rows],
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)

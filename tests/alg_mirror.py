@@ -72,6 +72,52 @@ def projector_mgs(Jc, thr_rel=1e-14):
     return np.eye(nv) - Q.T @ Q
 
 
+def mgs_rows(Jc, thr_rel=1e-14):
+    """The orthonormal rows Q of J_c's row space that K1's modified Gram-Schmidt takes (in row order)."""
+    X = np.array(Jc, dtype=np.float64)
+    k, nv = X.shape
+    nrm = np.einsum("ij,ij->i", X, X)
+    thr = thr_rel * thr_rel * (nrm.max() if k else 0.0)
+    taken = []
+    for p in range(k):
+        if not nrm[p] > thr:
+            continue
+        inv2 = 1.0 / nrm[p]
+        for j in range(p + 1, k):
+            X[j] = X[j] - ((X[p] @ X[j]) * inv2) * X[p]
+            nrm[j] = X[j] @ X[j]
+        taken.append(X[p] / np.sqrt(nrm[p]))
+    return np.array(taken).reshape(len(taken), nv)
+
+
+def nullspace_rows(Q):
+    """Zᵀ ((nv - r) x nv, orthonormal rows spanning null(Q)) as K1's Gram-only mode computes it, so that
+    ZZᵀ... Zᵀ Z = I - QᵀQ = P: the Householder vectors of Qᵀ's QR reconstructed by an unpivoted LU of
+    Qᵀ - diag(s) (s_j = -sign of the pivot, so every pivot has modulus |d_j| + 1 >= 1), tau_j = |d_j| + 1,
+    then row t of Zᵀ = (H_1 ... H_r e_{r+t})ᵀ, H_j = I - tau_j v_j v_jᵀ."""
+    Q = np.array(Q, dtype=np.float64)
+    r, nv = Q.shape
+    V = np.zeros((r, nv))
+    tau = np.zeros(r)
+    for j in range(r):
+        d = Q[j, j]
+        sg = 1.0 if d >= 0.0 else -1.0
+        v = np.zeros(nv)
+        v[j] = 1.0
+        v[j + 1:] = Q[j, j + 1:] / (d + sg)
+        for k in range(j + 1, r):
+            Q[k, j + 1:] -= Q[k, j] * v[j + 1:]
+        V[j], tau[j] = v, abs(d) + 1.0
+    Zt = np.zeros((nv - r, nv))
+    for t in range(nv - r):
+        y = np.zeros(nv)
+        y[r + t] = 1.0
+        for j in range(r - 1, -1, -1):
+            y -= tau[j] * (V[j] @ y) * V[j]
+        Zt[t] = y
+    return Zt
+
+
 def base_relative(model, d):
     """Poses relative to the free-flyer frame (the kernel's reference frame); v, a_gf unchanged."""
     for i in range(1, model.njoints):

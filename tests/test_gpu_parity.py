@@ -339,7 +339,8 @@ def test_reduced_precision_gram_matches_rounded_panel(robot, N):
     """The f32 / bf16 Gram kernels (each with its own super-tile deal and K3 reduction) against the exact
     Gram of the panel rounded the way K1 rounds it (f64 -> f32, then -> bf16, both RNE): what remains is only
     the kernels' f32 accumulation, so the bound is tight (1e-5 normwise), unlike the error against the f64
-    Gram that test_reduced_precision_gram reports.  Gram-only output vs the full path's f64 panel."""
+    Gram that test_reduced_precision_gram reports.  Gram-only output from the reference's P·A rows (the
+    GRAM_PROJECTOR rows, the same rows the full path's f64 panel holds) vs that panel."""
     import torch
     model = load_robot(robot)
     e = eng(robot)
@@ -354,7 +355,7 @@ def test_reduced_precision_gram_matches_rounded_panel(robot, N):
     for prec, pr in rounded.items():
         ref = (pr.T @ pr).cpu().numpy()
         g = e.alloc_gram_device(N)
-        e.build_gram_device(din, N, g, precision=prec)
+        e.build_gram_device(din, N, g, precision=prec, rows="projector")  # the same rows as the f64 panel
         torch.cuda.synchronize()
         G = g["gram"].cpu().numpy()
         err = np.linalg.norm(G - ref) / np.linalg.norm(ref)
@@ -458,3 +459,81 @@ def test_kernel_helper_on_device():
     out = out.reshape(64, 6)
     for lane in range(64):
         assert np.abs(out[lane] - Fw[:, lane % 10]).max() < 1e-13
+
+
+def _gram_only(e, din, N, prec="f64", rows="nullspace"):  # rows forced: "auto" picks projector for bf16
+    import torch
+    b = e.alloc_gram_device(N)
+    e.build_gram_device(din, N, b, precision=prec, rows=rows)
+    torch.cuda.synchronize()
+    return b["gram"].cpu().numpy()
+
+
+@pytest.mark.parametrize("robot,N,cfg", [("solo12", 2000, 0), ("spot", 20000, 1), ("g1_29dof", 5000, 2),
+                                         ("solo12_fixed", 2000, 3)])
+def test_gram_only_nullspace_rows(robot, N, cfg):
+    """Gram-only default: each sample contributes Zᵀ·A, its nv - rank(J_c) rows in an orthonormal basis Z of
+    null(J_c) (ZᵀZ = P, Householder-completed from K1's Gram-Schmidt basis), gathered by the Gram kernels
+    through k1s_row_list.  Against the reference's P·A rows (GRAM_PROJECTOR) and a sampled subset's oracle
+    Gram; bitwise repeatable; f32 / bf16 errors against f64 bounded as for the projector rows."""
+    import torch
+    from oracle.ref_c import COracle
+    model = load_robot(robot)
+    e = eng(robot)
+    d = generate(model, N, config_index=cfg)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    Gz, Gp = _gram_only(e, din, N), _gram_only(e, din, N, rows="projector")
+    err = rel(Gz, Gp)
+    assert err < 1e-10, err
+    assert np.array_equal(Gz, _gram_only(e, din, N))  # deterministic row list and summation order
+    assert np.array_equal(Gz, Gz.T)
+    idx = np.sort(np.random.default_rng(cfg).choice(N, 150, replace=False))
+    sub = {k: np.ascontiguousarray(d[k][:, idx]) for k in ("q", "dq", "ddq", "tau", "contact")}
+    o = COracle(model).build(sub["q"], sub["dq"], sub["ddq"], sub["tau"], sub["contact"], stacked=False)
+    Gs = _gram_only(e, torch.from_numpy(channel_block(sub)).cuda(), len(idx))
+    W = e.w
+    assert rel(Gs[:W, :W], o["gram"]) < TOL and rel(Gs[:W, W], o["Atb"]) < TOL
+    assert abs(Gs[W, W] - o["btb"]) <= TOL * o["btb"]
+    nrm = np.linalg.norm(Gz)
+    errs = {p: np.linalg.norm(_gram_only(e, din, N, prec=p) - Gz) / nrm for p in ("f32", "bf16")}
+    print(f"{robot} N={N} nullspace rows: vs projector rows {err:.2e}; f32 {errs['f32']:.2e} bf16 {errs['bf16']:.2e}")
+    assert errs["f32"] < 1e-5 and errs["bf16"] < 3e-2
+
+
+def test_gram_only_nullspace_degenerate_and_ill_conditioned():
+    """The nullspace rows on the hard contact cases, host entry point with EMIT_GRAM only (the Gram-only path)
+    against the numpy oracle's Gram of the reference's stacked P·A (1e-6): Spot with no / all / LOST=2 /
+    single feet, two contact slots on one foot (exactly dependent rows: rank 3 per duplicated pair), and
+    solo12_fixed on nearly straight knees (cond(J_c) up to 5e8, exactly singular legs, and four feet down:
+    J_c square and invertible, so a sample contributes no row at all)."""
+    import copy
+    model = load_robot("spot")
+    d = generate(model, 6, config_index=4)
+    cnt = np.stack([np.zeros(4), np.ones(4), 2 * np.ones(4), np.array([2, 0, 0, 0.0]), np.array([0, 0, 0, 1.0]),
+                    np.array([1, 2, 0, 1.0])], axis=1)
+    cases = [(model, eng("spot"), d, cnt)]
+    dup = copy.deepcopy(load_robot("spot"))
+    dup.end_effector_names[1] = dup.end_effector_names[0]
+    d2 = generate(dup, 16, config_index=2)
+    c2 = np.ones((4, 16))
+    c2[2:, ::2] = 0.0
+    cases.append((dup, Engine(dup), d2, c2))
+    fx = load_robot("solo12_fixed")
+    knees = [i for i, n in enumerate(fx.joint_names) if n.endswith("KFE")]
+    eps = [1e-2, 1e-4, 1e-6, 1e-8, 0.0]
+    pats = [[1, 1, 1, 0], [1, 0, 2, 0], [1, 1, 1, 1], [0, 1, 1, 1]]
+    n = len(eps) * len(pats)
+    d3 = generate(fx, n, config_index=3)
+    c3 = np.zeros((4, n))
+    for s in range(n):
+        for j in knees:
+            d3["q"][fx.idx_q[j], s] = eps[s % len(eps)]
+        c3[:, s] = pats[s // len(eps)]
+    cases.append((fx, eng("solo12_fixed"), d3, c3))
+    for m, e, dd, c in cases:
+        only = e.build(dd["q"], dd["dq"], dd["ddq"], dd["tau"], c, EMIT_GRAM)
+        Y, t = ref.get_projected_y_tau(m, dd["q"], dd["dq"], dd["ddq"], dd["tau"], c)
+        Bv, Bc = ref.get_projected_friction_regressors(m, dd["q"], dd["dq"], dd["ddq"], c)
+        G, g, btb, rows = ref.normal_equations(Y, t, Bv, Bc)
+        assert rel(only["gram"], G) < TOL and rel(only["Atb"], g) < TOL, m.robot_name
+        assert abs(only["btb"] - btb) <= TOL * abs(btb) and only["num_rows"] == rows

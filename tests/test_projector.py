@@ -74,3 +74,31 @@ def test_projector_identities():
     assert np.abs(P @ P - P).max() < 1e-13
     assert np.abs(J @ P).max() < 1e-13
     assert abs(np.trace(P) - 29) < 1e-12
+
+
+@pytest.mark.parametrize("nv,k", [(18, 12), (18, 6), (35, 6), (35, 3), (18, 0)])
+def test_nullspace_rows_factor_the_projector(nv, k):
+    """Gram-only mode (north_star "batched QR/nullspace"): K1 emits Zᵀ·A, nv - rank(J_c) rows
+    instead of P·A's nv, with Zᵀ from the Householder reconstruction of the MGS basis (tests/alg_mirror.py).
+    ZᵀZ = P (so Σ (ZᵀA)ᵀ(ZᵀA) = Σ AᵀPA, the same Gram), ZZᵀ = I, and Z ⊥ J_c; also for dependent rows and
+    for well- and ill-conditioned J_c, against the reference's pinv projector."""
+    rng = np.random.default_rng(nv + k)
+    for trial in range(20):
+        J = rng.standard_normal((k, nv))
+        if trial % 3 == 1 and k >= 6:
+            J[k - 3:] = 2.0 * J[:3] - J[3:6]  # three exactly dependent rows: rank k - 3
+        if trial % 3 == 2 and k > 0:
+            J, _ = with_singular_values(rng, k, nv, 3.0 * np.logspace(0, -6, k))
+        # cond(J_c) = 1e6 on the third kind: MGS's Q is orthonormal to ~eps·cond only, and Z inherits that
+        # (the same order as P = I - QᵀQ's own distance to the exact projector, test above)
+        tol = 1e-9 if trial % 3 == 2 else 1e-13
+        Q = am.mgs_rows(J)
+        Zt = am.nullspace_rows(Q)
+        r = Q.shape[0]
+        assert Zt.shape == (nv - r, nv)
+        P = am.projector_mgs(J)
+        assert np.abs(Zt.T @ Zt - P).max() < tol
+        assert np.abs(Zt @ Zt.T - np.eye(nv - r)).max() < tol
+        if k:
+            assert np.abs(Zt @ Q.T).max() < tol
+            assert np.abs(Zt.T @ Zt - pinv_projector(J)).max() < 1e-9
