@@ -48,11 +48,15 @@ struct sysid_engine {
   K1Params kp{};
   uint32_t* d_mimg = nullptr;
   unsigned long long* d_work = nullptr;  // K1 sample counter of the host-API paths (engine-owned buffers)
-  int k1_waves = 4, k1_blocks_per_cu = 1, k1_maxch_tpl = 4, k1_variant = 0;
-  size_t k1_lds = 0;
-  // K1 of the Gram-only nullspace mode (CMP instantiations, always the plain layout): its own launch shape
-  int k1c_variant = 0, k1c_waves = 4, k1c_blocks_per_cu = 1, k1c_wave_dbl = 0;
-  size_t k1c_lds = 0;
+  // a K1 launch shape: the instantiation (variant), its workgroup (waves), resident workgroups per CU, dynamic
+  // LDS, per-sample LDS doubles and layout switches (pov: P overlay, qf: Q-form without a P slot)
+  struct K1Shape {
+    int variant = 0, waves = 4, bpc = 1, wave_dbl = 0, pov = 0, qf = 0;
+    size_t lds = 0;
+  };
+  K1Shape k1m[3];  // projector rows, per panel element type (0 f64 / every stacked output, 1 f32, 2 bf16)
+  K1Shape k1c[3];  // the Gram-only nullspace mode (CMP instantiations of the plain layout), per element type
+  int k1_maxch_tpl = 4;
   // K2/K3 Gram tiling
   int ntc = 0;
   // super-tile deal per Gram arithmetic (0 f64, 1 f32, 2 bf16): each kernel's waves x slots per wave
@@ -126,7 +130,12 @@ constexpr int SYSID_K1_SPW_QUAD = 2, SYSID_K1_SPW_GEN = 1;
 // Chain slots of the nv = 18 kernel: the quadrupeds' legs are 3 revolute joints deep (3 measured 2% faster
 // than 4 on Spot: no dead slot in the column phase).
 constexpr int SYSID_K1_QCH = 3;
-enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16, K1_C12P, K1_C16P };  // ...P: the P-overlay layout (wave_layout pov)
+// ...P: the P-overlay layout (wave_layout pov); ...Q: the Q-form (at most K1_QF_KMAX contact rows, no P)
+enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16, K1_C12P, K1_C16P, K1_C4Q, K1_C12Q, K1_C16Q };
+int k1_qf_variant(int variant) {
+  return variant == K1_C4 ? K1_C4Q : variant == K1_C12 ? K1_C12Q : variant == K1_C16 ? K1_C16Q : -1;
+}
+bool k1_is_qf(int variant) { return variant == K1_C4Q || variant == K1_C12Q || variant == K1_C16Q; }
 int k1_pov_variant(int variant) { return variant == K1_C12 ? K1_C12P : variant == K1_C16 ? K1_C16P : -1; }
 bool k1_is_pov(int variant) { return variant == K1_C12P || variant == K1_C16P; }
 // a 12-slot instantiation for chains of 5..12 revolute joints (G1: 10; -2.8% against 16 slots)
@@ -153,6 +162,9 @@ const void* k1_fn_t(int variant) {
     case K1_C12: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT>);
     case K1_C12P: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 1>);
     case K1_C16P: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 1>);
+    case K1_C4Q: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>);
+    case K1_C12Q: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>);
+    case K1_C16Q: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>);
     default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT>);
   }
 }
@@ -174,6 +186,9 @@ void k1_launch_typed(sysid_engine* e, int variant, dim3 g1, dim3 b1, size_t lds,
 #define SYSID_K1_LAUNCH(MAXCH, NVC, SPW, POV)                                                                      \
   hipLaunchKernelGGL((k1_regressor_panel<MAXCH, NVC, SPW, OutT, POV, CMP>), g1, b1, lds, st, kp, e->d_mimg, d_in, N, \
                      ld, d_panel, ld_panel, work, dbg, rcount)
+#define SYSID_K1_LAUNCH_Q(MAXCH)                                                                                   \
+  hipLaunchKernelGGL((k1_regressor_panel<MAXCH, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>), g1, b1, lds, st, kp,         \
+                     e->d_mimg, d_in, N, ld, d_panel, ld_panel, work, dbg, rcount)
   switch (variant) {
     case K1_C4_NV18: SYSID_K1_LAUNCH(SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, 0); break;
     case K1_C4: SYSID_K1_LAUNCH(4, 0, SYSID_K1_SPW_GEN, 0); break;
@@ -185,8 +200,18 @@ void k1_launch_typed(sysid_engine* e, int variant, dim3 g1, dim3 b1, size_t lds,
     case K1_C16P:
       if constexpr (!CMP) SYSID_K1_LAUNCH(16, 0, SYSID_K1_SPW_GEN, 1);
       break;
+    case K1_C4Q:
+      if constexpr (!CMP) SYSID_K1_LAUNCH_Q(4);
+      break;
+    case K1_C12Q:
+      if constexpr (!CMP) SYSID_K1_LAUNCH_Q(12);
+      break;
+    case K1_C16Q:
+      if constexpr (!CMP) SYSID_K1_LAUNCH_Q(16);
+      break;
   }
 #undef SYSID_K1_LAUNCH
+#undef SYSID_K1_LAUNCH_Q
 }
 
 // The nullspace-mode instantiation of a variant (OutT of the Gram arithmetic), for the occupancy query.
@@ -214,14 +239,11 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
     kp.full = 1;
     kp.in_rows = e->in_lds;
   }
-  const int variant = cmp ? e->k1c_variant : e->k1_variant;
-  const int waves = cmp ? e->k1c_waves : e->k1_waves;
-  const int bpc = cmp ? e->k1c_blocks_per_cu : e->k1_blocks_per_cu;
-  const size_t lds = cmp ? e->k1c_lds : e->k1_lds;
-  if (cmp) {
-    kp.pov = 0;
-    kp.wave_dbl = e->k1c_wave_dbl;
-  }
+  const sysid_engine::K1Shape& K = cmp ? e->k1c[prec] : e->k1m[full ? 0 : prec];
+  const int variant = K.variant, waves = K.waves, bpc = K.bpc;
+  const size_t lds = K.lds;
+  kp.pov = K.pov;
+  kp.wave_dbl = K.wave_dbl;
   const int spw = k1_spw(variant);
   kp.rg = k1_row_groups(kp.NJ, 64 / spw);
   kp.out_cols = (int)std::min<int64_t>(ld_panel, prec == 0 ? e->ldp : ld_panel);
@@ -298,6 +320,13 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
       SYSID_K2_F64(NTC, KC)                                                                                       \
     } else if (prec == 1) {                                                                                       \
       SYSID_K2_F32(NTC, KC)                                                                                       \
+    } else if constexpr (k2b_supported(NTC)) {                                                                    \
+      if (gather)                                                                                                 \
+        hipLaunchKernelGGL((k2_gram_syrk_bf16_blk<NTC, true>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16, rows,    \
+                           ld_panel, ks, D.nslots, accumulate, slab, rowlist, d_rows);                            \
+      else                                                                                                        \
+        hipLaunchKernelGGL((k2_gram_syrk_bf16_blk<NTC>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16, rows,          \
+                           ld_panel, ks, D.nslots, accumulate, slab, nullptr, nullptr);                           \
     } else if (gather) {                                                                                          \
       hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC), true>), g2, dim3(64 * K2_BF16_WAVES), 0, \
                          st, p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist,  \
@@ -432,7 +461,11 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   const int prec = gram_prec(flags);
   // rows: nullspace (needs K1's register LU: at most K1_CMP_KMAX contact rows) or projector; by default the
   // nullspace rows for the f64 / f32 Grams and the projector rows for bf16 (include/sysid.h)
-  const bool want_ns = (flags & SYSID_GRAM_NULLSPACE) ? true : (flags & SYSID_GRAM_PROJECTOR) ? false : prec != 2;
+  // auto: nullspace rows unless the projector rows come from the Q-form K1 (G1 125k f32 9.68 vs 10.28 ms, bf16
+  // 4.90 vs 5.99 ms) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save)
+  const bool want_ns = (flags & SYSID_GRAM_NULLSPACE)   ? true
+                       : (flags & SYSID_GRAM_PROJECTOR) ? false
+                                                        : prec == 0 || (prec == 1 && !e->k1m[1].qf);
   const int cmp = want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
@@ -654,14 +687,14 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->ldp = (e->ncol + 1) & ~1;
   e->in_rows = in_rows;
   e->in_lds = in_lds;
-  e->k1_variant = k1_variant(maxch, nv, NJ - 1);
-  const int lhw = k1_layout_hw(e->k1_variant);
+  const int v0 = k1_variant(maxch, nv, NJ - 1);
+  const int lhw = k1_layout_hw(v0);
   const WLay WL0 = wave_layout(in_lds, nv, NJ, nc, lhw);
   // P overlay (wave_layout `pov`): runtime-nv kernels whose H1 is read from P (an even free-flyer offset), when
   // D's working set fits under P's slot and the passes landing on it fit the kernel's register buffer
   bool pov_ok = false;
   WLay WL1 = WL0;
-  if (lhw == 0 && k1_pov_variant(e->k1_variant) >= 0 && nff > 0 && (ff0 & 1) == 0) {
+  if (lhw == 0 && k1_pov_variant(v0) >= 0 && nff > 0 && (ff0 & 1) == 0) {
     const int pp = (nv * nv + 1) & ~1, qsize = WL0.P - WL0.Jc;
     if (qsize <= pp) {
       WL1 = wave_layout(in_lds, nv, NJ, nc, lhw, 1);
@@ -669,12 +702,14 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       pov_ok = passes - t0 <= K1_POV_BUF;
     }
   }
-  WLay WL = WL0;
+  // Q-form (no P): runtime-nv kernels with at most K1_QF_KMAX contact rows and <= 32 friction column pairs
+  const bool qf_ok = lhw == 0 && k1_qf_variant(v0) >= 0 && 3 * nc <= K1_QF_KMAX && nja <= 31;
+  const WLay WLQ = wave_layout(in_lds, nv, NJ, nc, 0, 0, 1);
   K1Params& kp = e->kp;
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;
   kp.wy = e->wy; kp.w = e->w; kp.ncol = e->ncol; kp.in_rows = in_rows; kp.maxch = maxch_tpl;
   kp.in_lds = in_lds; kp.full = 0;
-  kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL.total; kp.out_cols = e->ldp;
+  kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL0.total; kp.out_cols = e->ldp;
   kp.rg = k1_row_groups(NJ, 64);  // per launch: k1_row_groups(NJ, lanes per sample)
   kp.thr_rel = 1e-14;  // rank cut of the Gram-Schmidt projector (pinv: 1e-15 sigma_max)
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
@@ -802,6 +837,19 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     const int w = p == 2 ? K2_BF16_WAVES : k2_waves(e->ntc);
     const int sp = p == 0 ? k2_slots<double>(e->ntc) : p == 1 ? k2_slots<float>(e->ntc) : k2_bf16_spw(e->ntc);
     dealt[p] = deal(w, sp, D.ngroups, D.nsuper, D.nslots);
+    if (p == 2 && k2b_supported(e->ntc)) {
+      // the register-blocked bf16 kernel: one group, no super-tile slots, its waves' tiles in slab order
+      std::vector<int2> tl;
+      for (int w8 = 0; w8 < K2_BF16_WAVES; ++w8) {
+        const K2BRole R = k2b_role(e->ntc, w8);
+        for (int i = 0; i < R.nr; ++i)
+          for (int j = R.diag ? i : 0; j < R.nc; ++j) tl.push_back(int2{R.ra + i, R.ca + j});
+      }
+      D.ngroups = 1;
+      D.nsuper = 0;
+      D.nslots = (int)tl.size();
+      dealt[p].swap(tl);
+    }
   }
 
   hipError_t st = hipSetDevice(device);
@@ -819,70 +867,54 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     if (st == hipSuccess) st = hipMalloc(&t, dealt[p].size() * sizeof(int2));
     if (st == hipSuccess) st = hipMemcpy(t, dealt[p].data(), dealt[p].size() * sizeof(int2), hipMemcpyHostToDevice);
   }
-  // K1 shape: waves per workgroup that maximise resident waves per CU under the LDS budget
-  if (st == hipSuccess) {
+  // K1 shapes: per instantiation, the waves per workgroup that maximise resident waves per CU under the LDS
+  // budget.  Layout candidates of the projector rows: f64 (every stacked output) the plain layout (kept on ties)
+  // and the P overlay; f32 / bf16 chunk panels the Q-form when it applies (less arithmetic, no P slot; with f64
+  // elements its two column passes write each 80-byte body block in two pieces far apart in time, measured
+  // G1 125k K1 4.9 -> 7.2 ms, while bf16 gains 4.15 -> 3.38 ms).  The nullspace mode: CMP of the plain layout.
+  auto shape = [&](sysid_engine::K1Shape& K, int prec, int cmp, const int* vars, const WLay* wls, const int* povs,
+                   const int* qfs, int ncand) -> bool {
     int best = -1;
-    // layouts: the plain one first (kept on ties), then the P overlay; 8-wave workgroups for one-sample waves
-    const int v0 = e->k1_variant;
-    for (int ov = 0; ov < (pov_ok ? 2 : 1); ++ov) {
-      const WLay& wl = ov ? WL1 : WL0;
-      const int var = ov ? k1_pov_variant(v0) : v0;
+    for (int c = 0; c < ncand; ++c) {
+      const void* fn = cmp ? k1_fn_cmp(vars[c], prec) : k1_fn(vars[c], prec);
       for (int wv : {8, 4, 2, 1}) {
-        if (wv > K1_WAVES && !k1_is_pov(var)) continue;  // 8-wave workgroups: the overlay instantiations only
-        const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(var) * wl.total) * sizeof(double);
+        if (wv > K1_WAVES && !k1_is_pov(vars[c])) continue;  // 8-wave workgroups: the overlay instantiations only
+        const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(vars[c]) * wls[c].total) * sizeof(double);
         if (lds > 160 * 1024) continue;
-        // every panel element type's instantiation (the Gram-only f32 / bf16 paths launch their own): the
-        // shape must be resident for each of them
-        int nb = 1 << 30;
-        for (int pr = 0; pr < 3; ++pr) {
-          (void)hipFuncSetAttribute(k1_fn(var, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-          int x = 0;
-          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k1_fn(var, pr), 64 * wv, lds) != hipSuccess) x = 0;
-          nb = std::min(nb, x);
-        }
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * wv, lds) != hipSuccess) nb = 0;
         if (nb * wv > best) {
           best = nb * wv;
-          e->k1_waves = wv;
-          e->k1_blocks_per_cu = std::max(1, nb);
-          e->k1_lds = lds;
-          e->k1_variant = var;
-          WL = wl;
-          kp.pov = ov;
+          K.variant = vars[c];
+          K.waves = wv;
+          K.bpc = std::max(1, nb);
+          K.lds = lds;
+          K.wave_dbl = wls[c].total;
+          K.pov = povs[c];
+          K.qf = qfs[c];
         }
       }
     }
-    kp.wave_dbl = WL.total;
-    if (best <= 0) {
-      set_err(nullptr, SYSID_E_MODEL, "model needs too much LDS per sample (%zu B)", (size_t)WL.total * 8);
-      sysid_destroy(e);
-      return SYSID_E_MODEL;
-    }
-    for (int pr = 0; pr < 3 && st == hipSuccess; ++pr)
-      st = hipFuncSetAttribute(k1_fn(e->k1_variant, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1_lds);
-    // the Gram-only nullspace mode: its CMP instantiations of the plain-layout variant, shaped the same way
-    int bestc = -1;
-    e->k1c_variant = v0;
-    for (int wv : {4, 2, 1}) {
-      const size_t lds = (size_t)(MI.ndbl + wv * k1_spw(v0) * WL0.total) * sizeof(double);
-      if (lds > 160 * 1024) continue;
-      int nb = 1 << 30;
-      for (int pr = 0; pr < 3; ++pr) {
-        (void)hipFuncSetAttribute(k1_fn_cmp(v0, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        int x = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&x, k1_fn_cmp(v0, pr), 64 * wv, lds) != hipSuccess) x = 0;
-        nb = std::min(nb, x);
+    if (best <= 0) return false;
+    return hipFuncSetAttribute(cmp ? k1_fn_cmp(K.variant, prec) : k1_fn(K.variant, prec),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)K.lds) == hipSuccess;
+  };
+  if (st == hipSuccess) {
+    bool ok = true;
+    for (int pr = 0; pr < 3 && ok; ++pr) {
+      if (pr > 0 && qf_ok) {
+        const int vq[1] = {k1_qf_variant(v0)}, z[1] = {0}, one[1] = {1};
+        ok = shape(e->k1m[pr], pr, 0, vq, &WLQ, z, one, 1);
+      } else {
+        const int vp[2] = {v0, pov_ok ? k1_pov_variant(v0) : v0}, pv[2] = {0, 1}, z[2] = {0, 0};
+        const WLay wl[2] = {WL0, WL1};
+        ok = shape(e->k1m[pr], pr, 0, vp, wl, pv, z, pov_ok ? 2 : 1);
       }
-      if (nb * wv > bestc) {
-        bestc = nb * wv;
-        e->k1c_waves = wv;
-        e->k1c_blocks_per_cu = std::max(1, nb);
-        e->k1c_lds = lds;
-      }
+      const int z1[1] = {0};
+      if (ok) ok = shape(e->k1c[pr], pr, 1, &v0, &WL0, z1, z1, 1);
     }
-    e->k1c_wave_dbl = WL0.total;
-    for (int pr = 0; pr < 3 && st == hipSuccess; ++pr)
-      st = hipFuncSetAttribute(k1_fn_cmp(v0, pr), hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->k1c_lds);
-    if (bestc <= 0) {
+    if (!ok) {
       set_err(nullptr, SYSID_E_MODEL, "model needs too much LDS per sample (%zu B)", (size_t)WL0.total * 8);
       sysid_destroy(e);
       return SYSID_E_MODEL;
@@ -1277,7 +1309,7 @@ int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6) {
 
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
   if (!e || !offsets12) return SYSID_E_INVALID;
-  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant), e->kp.pov);
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1m[0].variant), e->k1m[0].pov, e->k1m[0].qf);
   const int o[12] = {L.in, L.body, L.W, L.Pt, L.Jw, L.pf, L.Jc, L.M, L.P, L.H1, L.tp, L.total};
   for (int k = 0; k < 12; ++k) offsets12[k] = o[k];
   return SYSID_OK;
@@ -1286,7 +1318,7 @@ int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12) {
 int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
                         const double* cnt, double* lds_image, int64_t image_doubles) {
   if (!e || !lds_image) return set_err(e, SYSID_E_INVALID, "null argument");
-  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1_variant), e->kp.pov);
+  const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1m[0].variant), e->k1m[0].pov, e->k1m[0].qf);
   if (image_doubles < L.total) return set_err(e, SYSID_E_INVALID, "image needs %d doubles", L.total);
   HIP_TRY(e, hipSetDevice(e->device));
   int rc = sysid_build(e, q, dq, ddq, tau, cnt, 1, 1, SYSID_EMIT_Y, nullptr, nullptr, nullptr, nullptr, nullptr,
@@ -1305,9 +1337,9 @@ int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, cons
 
 int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4) {
   if (!e || !cfg4) return SYSID_E_INVALID;
-  cfg4[0] = e->k1_waves;
-  cfg4[1] = e->k1_blocks_per_cu;
-  cfg4[2] = (int32_t)e->k1_lds;
+  cfg4[0] = e->k1m[0].waves;
+  cfg4[1] = e->k1m[0].bpc;
+  cfg4[2] = (int32_t)e->k1m[0].lds;
   cfg4[3] = e->k1_maxch_tpl;
   return SYSID_OK;
 }

@@ -86,7 +86,8 @@ struct WLay {
   int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, dqs, Z, total;
 };
 
-__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc, int hw, int pov = 0) {
+//   * with `nop` (the Q-form kernels, which never form P) there is no P slot at all.
+__host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc, int hw, int pov = 0, int nop = 0) {
   WLay l;
   const int k = 3 * nc;
   int o = 0;
@@ -115,6 +116,12 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc,
   l.Z = u0;                     // Q^T (orthonormal rows of J_c's row space), row r at r * 3 nc (W, Pt, pf
                                 // are dead by then)
   grow(u0 + r2(k * nv > k * k ? k * nv : k * k));
+  if (nop) {
+    l.P = l.Jc;                 // unused
+    l.H1 = D;                   // unused
+    l.total = o;
+    return l;
+  }
   if (hw > 0) {
     l.P = u0 - r2(margin);      // P = I - Q^T Q
     grow(l.P + r2(nv * nv));
@@ -449,15 +456,20 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 constexpr int K1_SEG_LOG = 10;  // samples per row-count segment of the CMP mode (1024)
 constexpr int K1_CMP_KMAX = 12;
   // CMP mode: at most 12 contact rows (4 contact frames; the host checks)
-template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0>
+// QF: the Q-form of the runtime-nv kernel for at most K1_QF_KMAX contact rows (G1: 6): P = I - QᵀQ is never
+// formed; the column phases use G_i[r] = [r in S_i] J_r - Σ_j Q_j[r] K_ij with K_ij = Σ_{d in S_i} Q_j[d] J_d
+// (S_i: the free-flyer and chain dofs of body i), k reads per row instead of a chain of P entries and axes.
+constexpr int K1_QF_KMAX = 6;
+template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0>
 // Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
 // The P overlay's instantiations run 8 one-sample waves per workgroup (one 8-wave workgroup per CU).
-__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 ? 2 : 1)
+__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 || QF ? 2 : 1)
 k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
                    int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
                    unsigned long long* __restrict__ work, double* __restrict__ dbg,
                    int* __restrict__ rcount) {
   static_assert(!(POV && CMP), "the nullspace mode runs the plain layout");
+  static_assert(!QF || (NVC == 0 && !POV && !CMP), "the Q-form is a runtime-nv, plain-layout kernel");
   extern __shared__ double smem[];
   const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
   {
@@ -492,7 +504,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   constexpr int HW = 64 / SPW;                       // lanes per sample
   const int half = lane / HW, hl = lane % HW;         // sample slot within the wave, lane within it
   static_assert(POV == 0 || NVC == 0, "the P overlay is a runtime-nv layout");
-  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0, POV);
+  const WLay L = wave_layout(kp.in_lds, nv, NJ, nc, NVC > 0 ? HW : 0, POV, QF);
   double* wr = smem + kp.mimg_dbl + (wave * SPW + half) * kp.wave_dbl;
   double* body = wr + L.body;
   double* Ws = wr + L.W;
@@ -812,7 +824,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     if (kp.full) {
       // get_full_regressor_force (src/sys_identification.py:391-399): no projection.  With the overlay P = I
       // is written after the tau column below (which reads J_c, under P's slot there).
-      if constexpr (!POV) {
+      if constexpr (!POV && !QF) {
         for (int e = hl; e < nv * nv; e += HW) {
           const int a = e / nv;
           Ps[e] = e - a * nv == a ? 1.0 : 0.0;
@@ -1069,7 +1081,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
           }
         }
         wsync();
-      } else {
+      } else if constexpr (!QF) {  // (the Q-form never forms P: its phases below read Q from J_c)
       // ---- P = I - Q^T Q  (Zt row a = column a of Q; J_c rows = rows of Q) ----
       if constexpr (NVC == 18 && HW == 32) {
         // Register-blocked: lane = (row pair, 6-column group), 27 lanes x 12 entries, every load before
@@ -1155,10 +1167,24 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 
     // ---- tp = P S^T tau  (+ J_c^T lambda in the full mode) ;  H1 = P[:, ff] J_w[:, ff]^T ----
     // tp first: in the full mode H1 may be stored over J_c (overlay layout), which the tau column reads.
+    // Q-form: tp = S^T tau - Qᵀ u, u_j = Q_j · S^T tau (u in the dead row-norm slots)
+    if constexpr (QF) {
+      if (!kp.full) {
+        for (int j = hl; j < k; j += HW) {
+          double acc = 0.0;
+          for (int jj = 0; jj < nja; ++jj) acc += Jc[j * nv + bd + jj] * tau[jj];
+          Ms[j] = acc;
+        }
+        wsync();
+      }
+    }
     for (int r = hl; r < nrows; r += HW) {
       double acc = 0.0;
-      if (POV && kp.full) {
+      if ((POV || QF) && kp.full) {
         acc = r >= bd && r < bd + nja ? tau[r - bd] : 0.0;  // P = I (not yet written)
+      } else if constexpr (QF) {
+        acc = r >= bd && r < bd + nja ? tau[r - bd] : 0.0;
+        for (int j = 0; j < k; ++j) acc -= Jc[j * nv + r] * Ms[j];
       } else {
 #pragma unroll 4
         for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
@@ -1197,7 +1223,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       }
       wsync();
     }
-    for (int e = hl; e < nrows * 6 && !h1_in_p; e += HW) {
+    for (int e = hl; e < nrows * 6 && !h1_in_p && !QF; e += HW) {
       const int r = e / 6, c = e - 6 * r;
       H1[e] = kp.has_ff ? Ps[r * nv + kp.ff0 + c] : 0.0;  // J_w[:, ff] = I (see h1_in_p)
     }
@@ -1367,6 +1393,94 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
         if (rho < rh) yrow(rho, hn, pn);
       }
+    } else if constexpr (QF) {
+      // Q-form: G_i[r] = [r in S_i] J_r - Σ_j Q_j[r] K_ij, K_ij = Σ_{d in S_i} Q_j[d] J_d, S_i = the free-flyer
+      // dofs (J = unit vectors in base coordinates: Q_j[ff0 + c]) and body i's chain; full mode: no Q (P = I).
+      const int kq = kp.full ? 0 : k;
+      for (int it = hl; it < nyi && valid; it += HW) {
+        const int g = it / nbody, i = it - g * nbody + 1;
+        const int r0 = g * nrows / kp.rg, r1 = (g + 1) * nrows / kp.rg;
+        // K first (F is not live yet), walking the chain in a rolled loop: unrolled over the chain slots the
+        // compiler kept every slot's loads in flight (~350 registers)
+        const int cl = chain_len[i];
+        unsigned long long smask = kp.has_ff ? (0x3Full << kp.ff0) : 0ull;
+        double Kq[K1_QF_KMAX][6];
+#pragma unroll
+        for (int j = 0; j < K1_QF_KMAX; ++j)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) Kq[j][c] = j < kq && kp.has_ff ? Jc[j * nv + kp.ff0 + c] : 0.0;
+#pragma unroll 1
+        for (int t = 0; t < cl; ++t) {
+          const int d = chain[i * kp.maxch + t];
+          smask |= 1ull << d;
+          const double2* jw = reinterpret_cast<const double2*>(Jws + 6 * d);
+          double a6[6];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const double2 v = jw[c];
+            a6[2 * c] = v.x;
+            a6[2 * c + 1] = v.y;
+          }
+#pragma unroll
+          for (int j = 0; j < K1_QF_KMAX; ++j) {
+            if (j < kq) {
+              const double qv = Jc[j * nv + d];
+#pragma unroll
+              for (int c = 0; c < 6; ++c) Kq[j][c] += qv * a6[c];
+            }
+          }
+        }
+        // two passes over the rows, one per half of the body block (registers: K + half a block): the
+        // inertia columns 4..9 (angular part of G only), then the mass / first-moment columns 0..3
+        const double* bi = body + BODY_STRIDE * i;
+        OutT* oi = out + 10 * (i - 1);
+        auto g_row = [&](int r, double* G, int c0) {  // G[c0..5] of row r
+          const bool inS = (smask >> r) & 1ull;
+          const double* jr = Jws + 6 * r;
+#pragma unroll
+          for (int c = c0; c < 6; ++c) G[c] = inS ? jr[c] : 0.0;
+#pragma unroll
+          for (int j = 0; j < K1_QF_KMAX; ++j) {
+            if (j < kq) {
+              const double qr = Jc[j * nv + r];
+#pragma unroll
+              for (int c = c0; c < 6; ++c) G[c] -= qr * Kq[j][c];
+            }
+          }
+        };
+        {
+          double FB[18];
+          body_block_inertia(bi, FB);
+#pragma unroll 1
+          for (int r = r0; r < r1; ++r) {
+            double G[6];
+            g_row(r, G, 3);
+            double y[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) y[c] = G[3] * FB[3 * c] + G[4] * FB[3 * c + 1] + G[5] * FB[3 * c + 2];
+            OutT* o2 = oi + (int64_t)r * ldp + 4;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) panel_store(o2 + 2 * c, y[2 * c], y[2 * c + 1]);
+          }
+        }
+        {
+          double FA[24];
+          body_block_mass(bi, FA);
+#pragma unroll 1
+          for (int r = r0; r < r1; ++r) {
+            double G[6];
+            g_row(r, G, 0);
+            double y[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              y[c] = G[0] * FA[6 * c] + G[1] * FA[6 * c + 1] + G[2] * FA[6 * c + 2] + G[3] * FA[6 * c + 3] +
+                     G[4] * FA[6 * c + 4] + G[5] * FA[6 * c + 5];
+            OutT* o2 = oi + (int64_t)r * ldp;
+            panel_store(o2, y[0], y[1]);
+            panel_store(o2 + 2, y[2], y[3]);
+          }
+        }
+      }
     } else {
       for (int it = hl; it < nyi && valid; it += HW) {
         const int g = it / nbody, i = it - g * nbody + 1;
@@ -1411,13 +1525,39 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         }
         OutT* po = out + (int64_t)fg * ldp + kp.wy + 2 * m;  // advanced by NG rows per pass
         const int64_t pstep = (int64_t)NG * ldp;
-        for (int r = fg; r < nrows; r += NG, po += pstep) {
-          const double* pr = Ps + r * nv + bd;
-          const double t = tps[r];
-          double v2[2];
+        if constexpr (QF) {
+          // P[r, bd + j] = δ - Σ_i Q_i[r] Q_i[bd + j]: the lane's two columns of Q in registers
+          const int kq = kp.full ? 0 : k;
+          double qc[K1_QF_KMAX][2];
 #pragma unroll
-          for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pr[jc[u]] * sc[u] : (tcol[u] ? t : 0.0);  // pad: whole lines
-          panel_store(po, v2[0], v2[1]);
+          for (int j = 0; j < K1_QF_KMAX; ++j)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) qc[j][u] = j < kq ? Jc[j * nv + bd + jc[u]] : 0.0;
+          for (int r = fg; r < nrows; r += NG, po += pstep) {
+            double pe[2] = {r == bd + jc[0] ? 1.0 : 0.0, r == bd + jc[1] ? 1.0 : 0.0};
+#pragma unroll
+            for (int j = 0; j < K1_QF_KMAX; ++j) {
+              if (j < kq) {
+                const double qr = Jc[j * nv + r];
+                pe[0] -= qr * qc[j][0];
+                pe[1] -= qr * qc[j][1];
+              }
+            }
+            const double t = tps[r];
+            double v2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pe[u] * sc[u] : (tcol[u] ? t : 0.0);
+            panel_store(po, v2[0], v2[1]);
+          }
+        } else {
+          for (int r = fg; r < nrows; r += NG, po += pstep) {
+            const double* pr = Ps + r * nv + bd;
+            const double t = tps[r];
+            double v2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pr[jc[u]] * sc[u] : (tcol[u] ? t : 0.0);  // pad: whole lines
+            panel_store(po, v2[0], v2[1]);
+          }
         }
       }
     } else {
@@ -2312,6 +2452,230 @@ k2_gram_syrk_bf16_tr(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp
       }
     }
   }
+}
+
+// K2 bf16, wide Grams of 16..23 tile columns: register-blocked tiles.  The super-tile kernel above reads two
+// A and two B fragments for every 2x2 super-tile and k-step: 1 fragment read per MFMA, and a
+// ds_read_b64_tr_b16 pair moves 1 KiB while the MFMA it feeds takes 16 cycles, so 8 waves of 10 super-tiles
+// asked 2.5k LDS cycles per 32-row k-step of a CU (conflicts included) for 1.25k cycles of MFMA per SIMD.  A
+// Gram's A and B fragments of one column block are the same registers (the MFMA takes both operands K-major),
+// so here every wave owns a block of tiles and reads each of its column blocks' fragments once per k-step:
+// three waves own the diagonal triangles of a three-way split of the columns (s = ceil(NTC/3) blocks: s
+// fragments feed s(s+1)/2 tiles), five the rectangles above them (nr + nc fragments feed nr x nc tiles).  G1
+// (23 tile columns): 84 fragment reads per CU and k-step instead of 312, per-SIMD MFMA loads 70/71/71/64
+// tiles (waves w and w + 4 share a SIMD).  The LDS image is row-major with a stride of 8 (mod 64) dwords, the
+// rows whose bit 3 is set in a second set of row slots 32 dwords further round the banks (k2b_row_off), so the
+// eight 32-byte row segments one 32-lane half of a transposed read touches fall on disjoint banks.
+struct K2BRole {
+  int diag, nr, nc, ra, ca;
+};
+__host__ __device__ constexpr K2BRole k2b_role(int ntc, int w) {
+  const int s = (ntc + 2) / 3, t = ntc - 2 * s;  // diagonal blocks [0,s) [s,2s) [2s,ntc)
+  const int h0 = (2 * s + 2) / 3, h1 = (2 * s - h0 + 1) / 2, h2 = 2 * s - h0 - h1;  // rows of [0,2s) x [2s,ntc)
+  const int b0 = (s + 1) / 2;                                                        // rows of [0,s) x [s,2s)
+  return w == 0   ? K2BRole{1, t, t, 2 * s, 2 * s}
+         : w == 1 ? K2BRole{1, s, s, 0, 0}
+         : w == 2 ? K2BRole{1, s, s, s, s}
+         : w == 3 ? K2BRole{0, b0, s, 0, s}
+         : w == 4 ? K2BRole{0, h0, t, 0, 2 * s}
+         : w == 5 ? K2BRole{0, h1, t, h0, 2 * s}
+         : w == 6 ? K2BRole{0, h2, t, h0 + h1, 2 * s}
+                  : K2BRole{0, s - b0, s, b0, s};
+}
+__host__ __device__ constexpr int k2b_ntiles(int ntc, int w) {
+  return k2b_role(ntc, w).diag ? k2b_role(ntc, w).nr * (k2b_role(ntc, w).nr + 1) / 2
+                               : k2b_role(ntc, w).nr * k2b_role(ntc, w).nc;
+}
+__host__ __device__ constexpr int k2b_base(int ntc, int w) { return w == 0 ? 0 : k2b_base(ntc, w - 1) + k2b_ntiles(ntc, w - 1); }
+__host__ __device__ constexpr int k2b_maxtiles(int ntc) {
+  int m = 0;
+  for (int w = 0; w < 8; ++w) m = k2b_ntiles(ntc, w) > m ? k2b_ntiles(ntc, w) : m;
+  return m;
+}
+__host__ __device__ constexpr bool k2b_supported(int ntc) { return ntc >= 16 && ntc <= 23; }
+// local tile index -> (I, J) of wave w (the slab / K3 tile order: wave by wave, row by row)
+__host__ __device__ constexpr int k2b_tile_index(int ntc, int w, int i, int j) {
+  return k2b_role(ntc, w).diag ? i * k2b_role(ntc, w).nr - i * (i - 1) / 2 + (j - i) : i * k2b_role(ntc, w).nc + j;
+}
+// LDS row stride of the block kernel in bytes: >= 16 NTC bf16, = 8 (mod 64) dwords
+__host__ __device__ constexpr int k2b_stride_bytes(int ntc) { return 4 * (((8 * ntc - 8 + 63) / 64) * 64 + 8); }
+// row r of a 64-row chunk: rows with bit 3 clear fill the first 32 row slots, rows with it set the next 32,
+// 128 bytes further on (so the two sets' banks differ by 32 dwords without a row running into the next)
+__host__ __device__ constexpr int k2b_row_off(int ntc, int r) {
+  return ((r >> 3) & 1) * (32 * k2b_stride_bytes(ntc) + 128) + ((r >> 4) * 8 + (r & 7)) * k2b_stride_bytes(ntc);
+}
+constexpr int K2B_KC = 64;  // rows per staged chunk (three buffers of 64 rows: G1 3 x 51.3 KB)
+
+template <int NTC, int W>
+__device__ __forceinline__ void k2b_mfma(const __bf16* cur, int lb, flt4 (&acc)[k2b_ntiles(NTC, W)]) {
+  constexpr K2BRole R = k2b_role(NTC, W);
+  constexpr int SE = k2b_stride_bytes(NTC) / 2;  // elements per LDS row
+#pragma unroll
+  for (int kk = 0; kk < K2B_KC; kk += 32) {
+    const __bf16* base = cur + (kk / 2) * SE + lb;  // k-step rows kk.. sit kk / 2 row slots on in both sets
+    if constexpr (R.diag) {
+      bf16x8 f[R.nr];
+#pragma unroll
+      for (int i = 0; i < R.nr; ++i) f[i] = k2_frag_tr(base + 16 * (R.ra + i), SE);
+#pragma unroll
+      for (int i = 0; i < R.nr; ++i)
+#pragma unroll
+        for (int j = i; j < R.nr; ++j) {
+          const int x = k2b_tile_index(NTC, W, i, j);
+          acc[x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[i], f[j], acc[x], 0, 0, 0);
+        }
+    } else {
+      bf16x8 a[R.nr];
+#pragma unroll
+      for (int i = 0; i < R.nr; ++i) a[i] = k2_frag_tr(base + 16 * (R.ra + i), SE);
+#pragma unroll
+      for (int j = 0; j < R.nc; ++j) {
+        const bf16x8 b = k2_frag_tr(base + 16 * (R.ca + j), SE);
+#pragma unroll
+        for (int i = 0; i < R.nr; ++i) {
+          const int x = i * R.nc + j;
+          acc[x] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[x], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+// One wave's whole pass (its role W fixed at compile time, so its accumulators are exactly its tiles): the
+// three-buffer LDS-DMA pipeline of k2_gram_syrk_bf16_tr, every wave staging KC / 8 rows of each chunk.
+template <int NTC, bool GATHER, int W>
+__device__ __forceinline__ void k2b_wave(char* lds, const __bf16* __restrict__ panel, int64_t r0, int64_t r1,
+                                         int64_t prows, int64_t ldp, int ks, int nslots, int accumulate,
+                                         double* __restrict__ slab, const int* __restrict__ rowlist, int lane) {
+  constexpr int K2W = K2_BF16_WAVES, KC = K2B_KC;
+  constexpr int BUFB = KC * k2b_stride_bytes(NTC) + 128;
+  constexpr int RPW = KC / K2W;
+  constexpr int NTW = k2b_ntiles(NTC, W);
+  const int rowbytes = (int)ldp * 2;  // <= 1 KiB: one DMA piece per row
+  auto dma_row = [&](const __bf16* src_row, char* dst_row) {
+    const int off = 16 * lane;
+    if (off < rowbytes)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(reinterpret_cast<const char*>(src_row) + off),
+                                       reinterpret_cast<void*>(dst_row), 16, 0, 0);
+  };
+  int gidx[RPW];
+  auto list_load = [&](int64_t c0) {
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int64_t x = c0 + W + K2W * q;
+        const int v = x < r1 ? rowlist[x] : 0;
+        gidx[q] = v >= 0 && v < prows ? v : 0;
+      }
+    }
+  };
+  auto dma_chunk = [&](int64_t c0, char* buf) {
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = W + K2W * q;
+      dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, buf + k2b_row_off(NTC, rr));
+    }
+  };
+  // this lane's fragment base (elements): row 8g + q of the k-step, columns 4p..4p+3 of a 16-column block
+  const int lb = k2b_row_off(NTC, 8 * (lane >> 4) + ((lane & 15) >> 2)) / 2 + 4 * (lane & 3);
+  flt4 acc[NTW];
+#pragma unroll
+  for (int x = 0; x < NTW; ++x) acc[x] = flt4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nfull = (r1 - r0) / KC;
+  char* b0 = lds;
+  char* b1 = lds + BUFB;
+  char* b2 = lds + 2 * BUFB;
+  list_load(r0);
+  if (nfull > 0) dma_chunk(r0, b0);
+  list_load(r0 + KC);
+  if (nfull > 1) {
+    dma_chunk(r0 + KC, b1);
+    list_load(r0 + 2 * KC);
+    k2_wait_vm<RPW>();  // chunk 0 landed (chunk 1 in flight)
+  } else {
+    k2_wait_vm<0>();
+  }
+  k2_barrier();
+  for (int64_t c = 0; c < nfull; ++c) {
+    const bool pre = c + 2 < nfull;
+    if (pre) {
+      dma_chunk(r0 + (c + 2) * KC, b2);
+      list_load(r0 + (c + 3) * KC);
+    }
+    k2b_mfma<NTC, W>(reinterpret_cast<const __bf16*>(b0), lb, acc);
+    if (pre) k2_wait_vm<RPW>();  // chunk c + 1 landed, chunk c + 2 stays in flight
+    else k2_wait_vm<0>();
+    k2_barrier();
+    char* t = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = t;
+  }
+  if (r0 + nfull * KC < r1) {  // the partial last chunk into b0 (its last reads retired at the barrier above)
+    const int64_t c0 = r0 + nfull * KC;
+    const int valid = (int)(r1 - c0);
+    list_load(c0);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = W + K2W * q;
+      char* dst = b0 + k2b_row_off(NTC, rr);
+      if (rr < valid) {
+        dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, dst);
+      } else {
+        for (int x = 16 * lane; x < rowbytes; x += 16 * 64)
+          *reinterpret_cast<uint4*>(dst + x) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    k2_wait_vm<0>();
+    k2_barrier();
+    k2b_mfma<NTC, W>(reinterpret_cast<const __bf16*>(b0), lb, acc);
+  }
+  constexpr int B = k2b_base(NTC, W);
+#pragma unroll
+  for (int x = 0; x < NTW; ++x) {
+    double* o = slab + ((size_t)ks * nslots + B + x) * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double* y = o + (4 * (lane >> 4) + j) * 16 + (lane & 15);
+      const double v = (double)acc[x][j];
+      *y = accumulate ? *y + v : v;
+    }
+  }
+}
+
+template <int NTC, bool GATHER = false>
+__global__ void __launch_bounds__(64 * K2_BF16_WAVES)
+k2_gram_syrk_bf16_blk(const __bf16* __restrict__ panel, int64_t rows, int64_t ldp, int ksplit, int nslots,
+                      int accumulate, double* __restrict__ slab, const int* __restrict__ rowlist,
+                      const int* __restrict__ d_rows) {
+  static_assert(k2b_supported(NTC), "16..23 tile columns");
+  constexpr int BUFB = K2B_KC * k2b_stride_bytes(NTC) + 128;  // bytes per LDS buffer
+  static_assert(3 * BUFB <= 160 * 1024, "three LDS buffers");
+  __shared__ __attribute__((aligned(16))) char lds[3 * BUFB];
+  const int ks = (int)blockIdx.x;
+  const int64_t prows = rows;
+  if constexpr (GATHER) rows = min((int64_t)__builtin_amdgcn_readfirstlane(*d_rows), prows);
+  const int64_t q4 = rows / 4;
+  const int64_t r0 = 4 * (q4 * ks / ksplit);
+  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  for (int x = 16 * threadIdx.x; x < 3 * BUFB; x += 16 * 64 * K2_BF16_WAVES)
+    *reinterpret_cast<uint4*>(lds + x) = make_uint4(0u, 0u, 0u, 0u);  // pads and columns >= ldp read as 0
+  __syncthreads();  // LDS zeroed (no DMA in flight yet)
+#define SYSID_K2B_WAVE(W) \
+  k2b_wave<NTC, GATHER, W>(lds, panel, r0, r1, prows, ldp, ks, nslots, accumulate, slab, rowlist, lane)
+  switch (wave) {  // every wave runs the same chunk loop and barriers with its own tiles
+    case 0: SYSID_K2B_WAVE(0); break;
+    case 1: SYSID_K2B_WAVE(1); break;
+    case 2: SYSID_K2B_WAVE(2); break;
+    case 3: SYSID_K2B_WAVE(3); break;
+    case 4: SYSID_K2B_WAVE(4); break;
+    case 5: SYSID_K2B_WAVE(5); break;
+    case 6: SYSID_K2B_WAVE(6); break;
+    default: SYSID_K2B_WAVE(7); break;
+  }
+#undef SYSID_K2B_WAVE
 }
 
 // K3, one pass: G = the sum of the ksplit slabs, in a fixed order, mirrored.  A workgroup of 16 waves owns 64
