@@ -62,6 +62,7 @@ struct sysid_engine {
   // super-tile deal per Gram arithmetic (0 f64, 1 f32, 2 bf16): each kernel's waves x slots per wave
   struct Deal {
     int ngroups = 0, nsuper = 0, nslots = 0;
+    int blk = 0;  // the register-blocked kernel (k2_gram_syrk_blk / _bf16_blk): one workgroup per CU
     int2* d_tiles = nullptr;  // [super slots | tile slots]
   } k2d[3];
   // host-API buffers (grow-only)
@@ -103,7 +104,7 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
 // chunks) run two workgroups per CU (measured: G1 K2 -11%, Spot unchanged net of the larger K3).
 int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
   // the bf16 kernel's large chunks take most of a CU's LDS: one workgroup per CU
-  const int mult = e->ntc >= 16 && prec != 2 ? 2 : 1;
+  const int mult = e->ntc >= 16 && prec != 2 && !e->k2d[prec].blk ? 2 : 1;
   int ks = std::max(1, mult * e->cus / std::max(1, e->k2d[prec].ngroups));
   const int64_t cap = std::max<int64_t>(1, rows / 64);  // >= 16 k-steps per workgroup
   return (int)std::min<int64_t>(ks, cap);
@@ -294,8 +295,17 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
   else                                                                                                              \
     hipLaunchKernelGGL((k2_gram_syrk_dma<T, NTC, KC>), g2, b2, 0, st, P, rows, ld_panel, D.d_tiles, D.ngroups,    \
                        ks, D.nslots, accumulate, slab, nullptr, nullptr);
+#define SYSID_K2_BLK(T, P, NTC)                                                                                    \
+  if (gather)                                                                                                       \
+    hipLaunchKernelGGL((k2_gram_syrk_blk<T, NTC, true>), g2, dim3(512), 0, st, P, rows, ld_panel, ks, D.nslots,     \
+                       accumulate, slab, rowlist, d_rows);                                                          \
+  else                                                                                                              \
+    hipLaunchKernelGGL((k2_gram_syrk_blk<T, NTC>), g2, dim3(512), 0, st, P, rows, ld_panel, ks, D.nslots,           \
+                       accumulate, slab, nullptr, nullptr);
 #define SYSID_K2_F64(NTC, KC)                                                                                      \
-  if constexpr (NTC >= 16) {                                \
+  if constexpr (k2b_supported(NTC)) {                                                                               \
+    SYSID_K2_BLK(double, p64, NTC)                                                                                  \
+  } else if constexpr (NTC >= 16) {                                \
     SYSID_K2_DMA_LAUNCH(double, p64, NTC, k2_dma_kc(NTC))                                                           \
   } else if (gather) {                                                                                              \
     hipLaunchKernelGGL((k2_gram_syrk_dma<double, NTC, k2_dma_kc(NTC), true>), g2, b2, 0, st, p64, rows, ld_panel,  \
@@ -305,7 +315,9 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
                        D.ngroups, ks, D.nslots, accumulate, slab);                                                  \
   }
 #define SYSID_K2_F32(NTC, KC) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                        \
-  if constexpr (NTC >= 16) {                                \
+  if constexpr (k2b_supported(NTC)) {                                                                               \
+    SYSID_K2_BLK(float, p32, NTC)                                                                                   \
+  } else if constexpr (NTC >= 16) {                                \
     SYSID_K2_DMA_LAUNCH(float, p32, NTC, 2 * k2_dma_kc(NTC))                                                        \
   } else if (gather) {                                                                                              \
     hipLaunchKernelGGL((k2_gram_syrk_dma<float, NTC, 2 * k2_dma_kc(NTC), true>), g2, b2, 0, st, p32, rows,         \
@@ -350,6 +362,7 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
 #undef SYSID_K2_F64
 #undef SYSID_K2_F32
 #undef SYSID_K2_DMA_LAUNCH
+#undef SYSID_K2_BLK
     default:
       return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
   }
@@ -837,15 +850,18 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     const int w = p == 2 ? K2_BF16_WAVES : k2_waves(e->ntc);
     const int sp = p == 0 ? k2_slots<double>(e->ntc) : p == 1 ? k2_slots<float>(e->ntc) : k2_bf16_spw(e->ntc);
     dealt[p] = deal(w, sp, D.ngroups, D.nsuper, D.nslots);
-    if (p == 2 && k2b_supported(e->ntc)) {
-      // the register-blocked bf16 kernel: one group, no super-tile slots, its waves' tiles in slab order
+    if (k2b_supported(e->ntc)) {
+      // the register-blocked kernels: no super-tile slots, the roles' tiles in slab order (8 roles per group;
+      // f64 two groups, f32 / bf16 one)
+      const int ng = p == 0 ? k2x_groups<double>() : 1;
       std::vector<int2> tl;
-      for (int w8 = 0; w8 < K2_BF16_WAVES; ++w8) {
-        const K2BRole R = k2b_role(e->ntc, w8);
+      for (int w8 = 0; w8 < 8 * ng; ++w8) {
+        const K2BRole R = p == 0 ? k2x_role<double>(e->ntc, w8) : k2b_role(e->ntc, w8);
         for (int i = 0; i < R.nr; ++i)
           for (int j = R.diag ? i : 0; j < R.nc; ++j) tl.push_back(int2{R.ra + i, R.ca + j});
       }
-      D.ngroups = 1;
+      D.blk = 1;
+      D.ngroups = ng;
       D.nsuper = 0;
       D.nslots = (int)tl.size();
       dealt[p].swap(tl);

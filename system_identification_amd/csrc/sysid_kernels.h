@@ -2678,6 +2678,240 @@ k2_gram_syrk_bf16_blk(const __bf16* __restrict__ panel, int64_t rows, int64_t ld
 #undef SYSID_K2B_WAVE
 }
 
+// K2 f32 / f64, wide Grams of 16..23 tile columns: the same register blocking on v_mfma_f32_16x16x4_f32 /
+// v_mfma_f64_16x16x4_f64 (4-row k-steps, one element per lane and fragment).  The super-tile kernels hold 16
+// super-tiles per workgroup, so G1's 78 took 5 groups and every panel row was staged 5 times (G1 20k f64 K2: 10
+// GB of staged rows in 1.67 ms).  f32 keeps its 276 tiles in one group (the bf16 roles: 4 accumulator VGPRs per
+// tile); an f64 tile takes 8, so f64 splits the Gram over two groups of 8 waves: four diagonal triangles of a
+// four-way split of the columns and the six rectangles above them cut in row halves (G1: per-SIMD loads
+// 36/36/36/33 and 33/33/33/36 tiles, 168 accumulator VGPRs at most).  LDS image: the f64 / f32 kernels' padded
+// row stride (k2_stride: the two rows of a 32-lane half of a fragment read on disjoint banks).
+__host__ __device__ constexpr int k2d_bstart(int ntc, int i) { return i * (ntc / 4) + (i < ntc % 4 ? i : ntc % 4); }
+__host__ __device__ constexpr int k2d_bsize(int ntc, int i) { return ntc / 4 + (i < ntc % 4 ? 1 : 0); }
+// rectangle (x, y) of the four-way split, row half h
+__host__ __device__ constexpr K2BRole k2d_rect(int ntc, int x, int y, int h) {
+  return K2BRole{0, h == 0 ? (k2d_bsize(ntc, x) + 1) / 2 : k2d_bsize(ntc, x) / 2, k2d_bsize(ntc, y),
+                 k2d_bstart(ntc, x) + (h == 0 ? 0 : (k2d_bsize(ntc, x) + 1) / 2), k2d_bstart(ntc, y)};
+}
+__host__ __device__ constexpr K2BRole k2d_role(int ntc, int w) {  // w = 8 group + wave; waves w, w + 4 share a SIMD
+  return w < 4     ? K2BRole{1, k2d_bsize(ntc, w), k2d_bsize(ntc, w), k2d_bstart(ntc, w), k2d_bstart(ntc, w)}
+         : w == 4  ? k2d_rect(ntc, 0, 3, 0)
+         : w == 5  ? k2d_rect(ntc, 0, 3, 1)
+         : w == 6  ? k2d_rect(ntc, 1, 3, 0)
+         : w == 7  ? k2d_rect(ntc, 0, 1, 0)
+         : w == 8  ? k2d_rect(ntc, 0, 1, 1)
+         : w == 9  ? k2d_rect(ntc, 0, 2, 0)
+         : w == 10 ? k2d_rect(ntc, 0, 2, 1)
+         : w == 11 ? k2d_rect(ntc, 1, 2, 0)
+         : w == 12 ? k2d_rect(ntc, 1, 3, 1)
+         : w == 13 ? k2d_rect(ntc, 2, 3, 0)
+         : w == 14 ? k2d_rect(ntc, 2, 3, 1)
+                   : k2d_rect(ntc, 1, 2, 1);
+}
+// per element type: roles (8 per group), groups, rows per staged chunk
+template <typename T> __host__ __device__ constexpr int k2x_groups() { return sizeof(T) == 8 ? 2 : 1; }
+template <typename T> __host__ __device__ constexpr K2BRole k2x_role(int ntc, int w) {
+  return sizeof(T) == 8 ? k2d_role(ntc, w) : k2b_role(ntc, w);
+}
+template <typename T> __host__ __device__ constexpr int k2x_ntiles(int ntc, int w) {
+  return k2x_role<T>(ntc, w).diag ? k2x_role<T>(ntc, w).nr * (k2x_role<T>(ntc, w).nr + 1) / 2
+                                  : k2x_role<T>(ntc, w).nr * k2x_role<T>(ntc, w).nc;
+}
+template <typename T> __host__ __device__ constexpr int k2x_base(int ntc, int w) {
+  return w == 0 ? 0 : k2x_base<T>(ntc, w - 1) + k2x_ntiles<T>(ntc, w - 1);
+}
+template <typename T> __host__ __device__ constexpr int k2x_kc(int ntc) {  // three buffers in 160 KB, 8 | KC
+  return (160 * 1024 / (3 * k2_stride(ntc) * (int)sizeof(T))) / 8 * 8 > 32 ? 32
+                                                                           : (160 * 1024 / (3 * k2_stride(ntc) * (int)sizeof(T))) / 8 * 8;
+}
+
+template <typename T, int NTC, int W>
+__device__ __forceinline__ void k2x_mfma(const T* cur, int lb, typename K2Acc<T>::type (&acc)[k2x_ntiles<T>(NTC, W)]) {
+  constexpr K2BRole R = k2x_role<T>(NTC, W);
+  constexpr int STRIDE = k2_stride(NTC), KC = k2x_kc<T>(NTC);
+  auto mm = [](T a, T b, typename K2Acc<T>::type c) {
+    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  };
+#pragma unroll
+  for (int kk = 0; kk < KC; kk += 4) {
+    const T* base = cur + kk * STRIDE + lb;
+    if constexpr (R.diag) {
+      T f[R.nr];
+#pragma unroll
+      for (int i = 0; i < R.nr; ++i) f[i] = base[16 * (R.ra + i)];
+#pragma unroll
+      for (int i = 0; i < R.nr; ++i)
+#pragma unroll
+        for (int j = i; j < R.nr; ++j) {
+          const int x = i * R.nr - i * (i - 1) / 2 + (j - i);
+          acc[x] = mm(f[i], f[j], acc[x]);
+        }
+    } else {
+      T a[R.nr];
+#pragma unroll
+      for (int i = 0; i < R.nr; ++i) a[i] = base[16 * (R.ra + i)];
+#pragma unroll
+      for (int j = 0; j < R.nc; ++j) {
+        const T b = base[16 * (R.ca + j)];
+#pragma unroll
+        for (int i = 0; i < R.nr; ++i) acc[i * R.nc + j] = mm(a[i], b, acc[i * R.nc + j]);
+      }
+    }
+  }
+}
+
+template <typename T, int NTC, bool GATHER, int W>
+__device__ __forceinline__ void k2x_wave(T* lds, const T* __restrict__ panel, int64_t r0, int64_t r1, int64_t prows,
+                                         int64_t ldp, int ks, int nslots, int accumulate, double* __restrict__ slab,
+                                         const int* __restrict__ rowlist, int wave, int lane) {
+  typedef typename K2Acc<T>::type accT;
+  constexpr int K2W = 8, KC = k2x_kc<T>(NTC), STRIDE = k2_stride(NTC);
+  constexpr int BUF = KC * STRIDE;
+  constexpr int RPW = KC / K2W;
+  constexpr int EB = (int)sizeof(T);
+  constexpr int NTW = k2x_ntiles<T>(NTC, W);
+  const int rowbytes = (int)ldp * EB;
+  const int np = (rowbytes + 1023) >> 10;  // 1 KiB pieces per row (wave-uniform, 1..3)
+  constexpr int NPMAX = (16 * NTC * EB + 1023) / 1024;
+  auto dma_row = [&](const T* src_row, T* dst_row) {
+    const char* src = reinterpret_cast<const char*>(src_row);
+    char* dst = reinterpret_cast<char*>(dst_row);
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) {
+      if (p < np) {
+        const int off = (p << 10) + 16 * lane;
+        if (off < rowbytes)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + off),
+                                           reinterpret_cast<void*>(dst + (p << 10)), 16, 0, 0);
+      }
+    }
+  };
+  int gidx[RPW];
+  auto list_load = [&](int64_t c0) {
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int64_t x = c0 + wave + K2W * q;
+        const int v = x < r1 ? rowlist[x] : 0;
+        gidx[q] = v >= 0 && v < prows ? v : 0;
+      }
+    }
+  };
+  auto dma_chunk = [&](int64_t c0, T* buf) {
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave + K2W * q;
+      dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, buf + rr * STRIDE);
+    }
+  };
+  const int lb = (lane >> 4) * STRIDE + (lane & 15);  // A/B fragment: k = lane >> 4, column lane & 15
+  accT acc[NTW];
+#pragma unroll
+  for (int x = 0; x < NTW; ++x) acc[x] = accT{0, 0, 0, 0};
+
+  const int64_t nfull = (r1 - r0) / KC;
+  T* b0 = lds;
+  T* b1 = lds + BUF;
+  T* b2 = lds + 2 * BUF;
+  list_load(r0);
+  if (nfull > 0) dma_chunk(r0, b0);
+  list_load(r0 + KC);
+  if (nfull > 1) {
+    dma_chunk(r0 + KC, b1);
+    list_load(r0 + 2 * KC);
+    k2_wait_chunk<RPW>(np);  // chunk 0 landed (chunk 1 in flight)
+  } else {
+    k2_wait_vm<0>();
+  }
+  k2_barrier();
+  for (int64_t c = 0; c < nfull; ++c) {
+    const bool pre = c + 2 < nfull;
+    if (pre) {
+      dma_chunk(r0 + (c + 2) * KC, b2);
+      list_load(r0 + (c + 3) * KC);
+    }
+    k2x_mfma<T, NTC, W>(b0, lb, acc);
+    if (pre) k2_wait_chunk<RPW>(np);  // chunk c + 1 landed, chunk c + 2 stays in flight
+    else k2_wait_vm<0>();
+    k2_barrier();
+    T* t = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = t;
+  }
+  if (r0 + nfull * KC < r1) {  // the partial last chunk into b0
+    const int64_t c0 = r0 + nfull * KC;
+    const int valid = (int)(r1 - c0);
+    list_load(c0);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave + K2W * q;
+      T* dst = b0 + rr * STRIDE;
+      if (rr < valid) {
+        dma_row(panel + (GATHER ? (int64_t)gidx[q] : c0 + rr) * ldp, dst);
+      } else {
+        for (int x = 16 * lane; x < rowbytes; x += 16 * 64)
+          *reinterpret_cast<uint4*>(reinterpret_cast<char*>(dst) + x) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    k2_wait_vm<0>();
+    k2_barrier();
+    k2x_mfma<T, NTC, W>(b0, lb, acc);
+  }
+  constexpr int B = k2x_base<T>(NTC, W);
+  // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
+#pragma unroll
+  for (int x = 0; x < NTW; ++x) {
+    double* o = slab + ((size_t)ks * nslots + B + x) * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = EB == 8 ? (lane >> 4) + 4 * j : 4 * (lane >> 4) + j;
+      double* y = o + row * 16 + (lane & 15);
+      const double v = (double)acc[x][j];
+      *y = accumulate ? *y + v : v;
+    }
+  }
+}
+
+template <typename T, int NTC, bool GATHER = false>
+__global__ void __launch_bounds__(512)
+k2_gram_syrk_blk(const T* __restrict__ panel, int64_t rows, int64_t ldp, int ksplit, int nslots, int accumulate,
+                 double* __restrict__ slab, const int* __restrict__ rowlist, const int* __restrict__ d_rows) {
+  static_assert(k2b_supported(NTC), "16..23 tile columns");
+  constexpr int KC = k2x_kc<T>(NTC), BUF = KC * k2_stride(NTC);
+  static_assert(KC % 8 == 0 && KC >= 8 && 3 * BUF * (int)sizeof(T) <= 160 * 1024, "three LDS buffers");
+  __shared__ __attribute__((aligned(16))) T lds[3 * BUF];
+  int group, ks;
+  k2_block_coords(k2x_groups<T>(), group, ks);
+  const int64_t prows = rows;
+  if constexpr (GATHER) rows = min((int64_t)__builtin_amdgcn_readfirstlane(*d_rows), prows);
+  const int64_t q4 = rows / 4;
+  const int64_t r0 = 4 * (q4 * ks / ksplit);
+  const int64_t r1 = ks + 1 == ksplit ? rows : 4 * (q4 * (ks + 1) / ksplit);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  for (int x = threadIdx.x; x < 3 * BUF; x += 512) lds[x] = (T)0;  // columns >= ldp read as 0
+  __syncthreads();
+#define SYSID_K2X_WAVE(W)                                                                                        \
+  case W:                                                                                                        \
+    k2x_wave<T, NTC, GATHER, W>(lds, panel, r0, r1, prows, ldp, ks, nslots, accumulate, slab, rowlist, wave, lane); \
+    break;
+  switch (8 * group + wave) {
+    SYSID_K2X_WAVE(0) SYSID_K2X_WAVE(1) SYSID_K2X_WAVE(2) SYSID_K2X_WAVE(3)
+    SYSID_K2X_WAVE(4) SYSID_K2X_WAVE(5) SYSID_K2X_WAVE(6) SYSID_K2X_WAVE(7)
+    default:
+      if constexpr (k2x_groups<T>() == 2) {
+        switch (8 * group + wave) {
+          SYSID_K2X_WAVE(8) SYSID_K2X_WAVE(9) SYSID_K2X_WAVE(10) SYSID_K2X_WAVE(11)
+          SYSID_K2X_WAVE(12) SYSID_K2X_WAVE(13) SYSID_K2X_WAVE(14)
+          default: k2x_wave<T, NTC, GATHER, 15>(lds, panel, r0, r1, prows, ldp, ks, nslots, accumulate, slab, rowlist, wave, lane);
+        }
+      }
+      break;
+  }
+#undef SYSID_K2X_WAVE
+}
+
 // K3, one pass: G = the sum of the ksplit slabs, in a fixed order, mirrored.  A workgroup of 16 waves owns 64
 // consecutive entries of one tile slot (so a dead slot drops the whole workgroup); wave w sums slabs w, w + 16,
 // ... with eight loads in flight per lane, and the 16 wave sums are added in LDS as a fixed pairwise tree.
