@@ -368,6 +368,12 @@ class Engine:
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)
 
+    def k1_config(self) -> list:
+        """K1 launch shape of the f64 panel [waves per workgroup, workgroups per CU, LDS bytes, chain slots]."""
+        cfg = (ctypes.c_int32 * 4)()
+        self._check(self.lib.sysid_debug_k1_config(self._h, cfg))
+        return list(cfg)
+
     def time_stages(self, d_in, N: int, flags: int, bufs: dict, iters: int = 10) -> list:
         """Mean ms per step in each stage [regressor/projector, Gram SYRK, Gram reduce] (HIP events).  With
         Gram-only buffers (alloc_gram_device: no "panel") the chunked Gram-only path is timed, its chunks summed."""

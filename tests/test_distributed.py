@@ -120,9 +120,17 @@ def test_gloo_uneven_shards_allreduce(tmp_path):
 
 
 def test_row_count_survives_the_float_buffer():
-    """The row count rides in the all-reduced float64 buffer: exact for any count below 2^53."""
-    from system_identification_amd.distributed import pack_normal_equations
-    ne = {"gram": np.eye(3), "Atb": np.zeros(3), "btb": 0.0, "num_rows": 2 ** 40 + 12345}
-    buf, rows = pack_normal_equations(ne)
-    flat = np.concatenate([buf.reshape(-1), [float(rows)]])
-    assert int(round((flat + flat)[-1])) == 2 * (2 ** 40 + 12345)
+    """The row count rides in the all-reduced float64 buffer: exact for any count below 2^53, through
+    allreduce_normal_equations itself (a one-rank gloo group)."""
+    import tempfile
+    import torch.distributed as dist
+    from system_identification_amd.distributed import allreduce_normal_equations
+    ne = {"gram": np.eye(3), "Atb": np.arange(3.0), "btb": 2.5, "num_rows": 2 ** 40 + 12345}
+    with tempfile.TemporaryDirectory() as tmp:
+        dist.init_process_group("gloo", init_method=f"file://{tmp}/rdv", rank=0, world_size=1)
+        try:
+            out = allreduce_normal_equations(ne)
+        finally:
+            dist.destroy_process_group()
+    assert out["num_rows"] == 2 ** 40 + 12345 and isinstance(out["num_rows"], int)
+    assert np.array_equal(out["gram"], ne["gram"]) and np.array_equal(out["Atb"], ne["Atb"]) and out["btb"] == 2.5

@@ -45,8 +45,10 @@ def check_blocks(out, Y, t, Bv, Bc, model, q, dq, ddq, tau):
 
 
 @pytest.mark.parametrize("robot,N,cfg", [("solo12", 48, 0), ("spot", 64, 1), ("g1_29dof", 24, 2),
-                                         ("solo12_fixed", 48, 3)])
+                                         ("solo12_fixed", 48, 3), ("snake14", 40, 5)])
 def test_panel_and_gram_vs_oracle(robot, N, cfg):
+    """snake14 (an authored robot with a 14-joint tail, tools/make_robots.py) is the one model whose chains
+    need the 16-slot K1 instantiations: K1_C16P here, K1_C16Q in the reduced-precision tests below."""
     model = load_robot(robot)
     d = generate(model, N, config_index=cfg)
     out = eng(robot).build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_ALL)
@@ -58,6 +60,8 @@ def test_panel_and_gram_vs_oracle(robot, N, cfg):
     assert rel(out["Atb"], g) < TOL
     assert abs(out["btb"] - btb) <= TOL * abs(btb)
     assert out["num_rows"] == rows
+    if robot == "snake14":
+        assert eng(robot).k1_config()[3] == 16  # the 16-slot chain instantiation ran
 
 
 @pytest.mark.parametrize("robot", ["solo12", "spot", "g1_29dof", "solo12_fixed"])
@@ -334,7 +338,7 @@ def test_reduced_precision_gram(robot, N):
     assert np.array_equal(out["f32"], out["f32"].T) and np.array_equal(out["bf16"], out["bf16"].T)
 
 
-@pytest.mark.parametrize("robot,N", [("spot", 20000), ("g1_29dof", 5000)])
+@pytest.mark.parametrize("robot,N", [("spot", 20000), ("g1_29dof", 5000), ("snake14", 4000)])
 def test_reduced_precision_gram_matches_rounded_panel(robot, N):
     """The f32 / bf16 Gram kernels (each with its own super-tile deal and K3 reduction) against the exact
     Gram of the panel rounded the way K1 rounds it (f64 -> f32, then -> bf16, both RNE): what remains is only
@@ -470,7 +474,7 @@ def _gram_only(e, din, N, prec="f64", rows="nullspace"):  # rows forced: "auto" 
 
 
 @pytest.mark.parametrize("robot,N,cfg", [("solo12", 2000, 0), ("spot", 20000, 1), ("g1_29dof", 5000, 2),
-                                         ("solo12_fixed", 2000, 3)])
+                                         ("solo12_fixed", 2000, 3), ("snake14", 3000, 6)])
 def test_gram_only_nullspace_rows(robot, N, cfg):
     """Gram-only default: each sample contributes Zᵀ·A, its nv - rank(J_c) rows in an orthonormal basis Z of
     null(J_c) (ZᵀZ = P, Householder-completed from K1's Gram-Schmidt basis), gathered by the Gram kernels

@@ -24,7 +24,63 @@ SOURCES = {  # name: (urdf, yaml, floating_base)
 }
 
 
+def _link(name, mass, com, diag):
+    ix, iy, iz = diag
+    return (f'  <link name="{name}"><inertial><origin xyz="{com[0]} {com[1]} {com[2]}" rpy="0 0 0"/>'
+            f'<mass value="{mass}"/><inertia ixx="{ix}" ixy="0.001" ixz="0" iyy="{iy}" iyz="0.0005" izz="{iz}"/>'
+            f'</inertial></link>')
+
+
+def _joint(name, parent, child, xyz, axis, jtype="revolute"):
+    lim = '<limit lower="-1.2" upper="1.2" effort="50" velocity="10"/>' if jtype == "revolute" else ""
+    ax = f'<axis xyz="{axis}"/>' if jtype == "revolute" else ""
+    return (f'  <joint name="{name}" type="{jtype}"><parent link="{parent}"/><child link="{child}"/>'
+            f'<origin xyz="{xyz}" rpy="0.1 0 0"/>{ax}{lim}</joint>')
+
+
+def snake14():
+    """An authored test robot (no reference input): a floating trunk on two 3-joint legs with a 14-joint tail,
+    so the runtime-nv K1 takes its 16-slot chain instantiations (C16P for f64, C16Q for the f32 / bf16 chunk
+    panels) that the reference's robots never select."""
+    L = ['<?xml version="1.0"?>', '<robot name="snake14">', _link("trunk", 4.0, (0.01, 0.0, 0.02), (0.05, 0.08, 0.09))]
+    for side, y in (("left", 0.12), ("right", -0.12)):
+        prev = "trunk"
+        for k, (ax, xyz) in enumerate((("0 0 1", f"0.1 {y} 0"), ("0 1 0", "0 0 -0.05"), ("0 1 0", "0 0 -0.2"))):
+            ln = f"{side}_leg{k}"
+            L.append(_link(ln, 0.6 - 0.1 * k, (0.0, 0.01, -0.08), (0.004, 0.005, 0.002)))
+            L.append(_joint(f"{side}_leg{k}_joint", prev, ln, xyz, ax))
+            prev = ln
+        L.append(_link(f"{side}_foot", 0.05, (0, 0, 0), (1e-5, 1e-5, 1e-5)))
+        L.append(_joint(f"{side}_foot_fixed", prev, f"{side}_foot", "0 0 -0.2", "", "fixed"))
+    prev = "trunk"
+    for k in range(14):
+        ln = f"tail{k:02d}"
+        L.append(_link(ln, 0.3 - 0.01 * k, (-0.04, 0.0, 0.005), (0.0008, 0.001, 0.0011)))
+        L.append(_joint(f"tail{k:02d}_joint", prev, ln, "-0.2 0 0" if k == 0 else "-0.08 0 0",
+                        ("0 0 1", "0 1 0", "1 0 0")[k % 3]))
+        prev = ln
+    L.append("</robot>")
+    urdf = os.path.join(ROBOT_DIR, "snake14.urdf")
+    with open(urdf, "w") as fh:
+        fh.write("\n".join(L) + "\n")
+    links = ["trunk"] + [f"{s}_leg{k}" for s in ("left", "right") for k in range(3)] + [f"tail{k:02d}" for k in range(14)]
+    cfg = os.path.join(ROBOT_DIR, "snake14_config.yaml")
+    with open(cfg, "w") as fh:
+        fh.write("# Authored test robot (tools/make_robots.py snake14): contacts are the two feet.\n")
+        fh.write('robot:\n  name: "snake14"\n  mass: 9.57\n  end_effectors_frame_names:\n')
+        fh.write('    - "left_foot"\n    - "right_foot"\n  link_names:\n')
+        for ln in links:
+            fh.write(f'    - "{ln}"\n')
+    m = build_model_from_urdf(urdf, cfg, floating_base=True)
+    out = os.path.join(ROBOT_DIR, "snake14.json")
+    m.save_json(out)
+    print(f"snake14: nq={m.nq} nv={m.nv} nb={m.nb} n_ee={m.n_ee} -> {out}")
+
+
 def main():
+    snake14()
+    if not os.path.isdir(REF):
+        return
     for name, (urdf, cfg, floating) in SOURCES.items():
         cfg_path = cfg if os.path.isabs(cfg) else os.path.join(REF, cfg)
         m = build_model_from_urdf(os.path.join(REF, urdf), cfg_path, floating_base=floating)

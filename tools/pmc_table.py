@@ -1,10 +1,11 @@
-"""Average per-dispatch PMC values per kernel from rocprofv3 counter_collection CSVs."""
-import collections, csv, re, sys
+"""Average per-dispatch PMC values per kernel from rocprofv3 counter_collection CSVs (dev tool).
+usage: python tools/pmc_table.py <pass dir> [<pass dir> ...]   (each holding run_counter_collection.csv)"""
+import collections, csv, sys
 agg = collections.defaultdict(list)
 for d in sys.argv[1:]:
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        m = re.search(r"::(\w+?)(<\w+>)?\(", r["Kernel_Name"])
-        k = (m.group(1) if m else r["Kernel_Name"][:30])
+        name = r["Kernel_Name"]
+        k = name.split("(")[0].split("<")[0].replace("void ", "").split("::")[-1]
         agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
 cur = None
 for (k, c), v in sorted(agg.items()):
