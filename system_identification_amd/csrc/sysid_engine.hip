@@ -716,7 +716,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     }
   }
   // Q-form (no P): runtime-nv kernels with at most K1_QF_KMAX contact rows and <= 32 friction column pairs
-  const bool qf_ok = lhw == 0 && k1_qf_variant(v0) >= 0 && 3 * nc <= K1_QF_KMAX && nja <= 31;
+  const bool qf_ok = lhw == 0 && k1_qf_variant(v0) >= 0 && nc > 0 && 3 * nc <= K1_QF_KMAX && nja <= 31;
   const WLay WLQ = wave_layout(in_lds, nv, NJ, nc, 0, 0, 1);
   K1Params& kp = e->kp;
   kp.nq = nq; kp.nv = nv; kp.NJ = NJ; kp.nc = nc; kp.bd = bd; kp.nj = nja; kp.maxdepth = maxdepth;

@@ -354,9 +354,14 @@ __device__ __forceinline__ void panel_store(float* p, double a, double b) {
   *reinterpret_cast<float2*>(p) = make_float2((float)a, (float)b);
 }
 __device__ __forceinline__ void panel_store(__bf16* p, double a, double b) {
+  // RNE to f32, then RNE to bf16 (v_cvt_pk_bf16_f32).  The empty asm keeps the f32 values: without it the two
+  // truncations fold into one f64 -> bf16 rounding, which the compiler emulates with a round-to-odd sequence
+  // of ~10 VALU per value (G1's Q-form K1: ~1.7k VALU per sample)
+  float fa = (float)a, fb = (float)b;
+  asm volatile("" : "+v"(fa), "+v"(fb));
   bf16x2_t v;
-  v[0] = (__bf16)(float)a;  // RNE to f32, then RNE to bf16 (v_cvt_pk_bf16_f32)
-  v[1] = (__bf16)(float)b;
+  v[0] = (__bf16)fa;
+  v[1] = (__bf16)fb;
   *reinterpret_cast<bf16x2_t*>(p) = v;
 }
 
@@ -601,6 +606,12 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   // issue priority: the column phase runs at 0, everything else at 2, so a wave in a latency-bound phase
   // issues first when its operands arrive (K1 -1 to -2%, Spot and G1)
   __builtin_amdgcn_s_setprio(2);
+  if constexpr (QF) {
+    // the Q-form's column phases read all K1_QF_KMAX row slots of J_c and multiply the ones past the sample's
+    // k by zero: rows not yet written must hold finite values (later samples leave finite rows behind)
+    for (int x = hl; x < 3 * nc * nv; x += HW) Jc[x] = 0.0;
+    wsync();
+  }
   const int hl_outer = hl;
   while (s < N) {
     // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
@@ -1396,7 +1407,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     } else if constexpr (QF) {
       // Q-form: G_i[r] = [r in S_i] J_r - Σ_j Q_j[r] K_ij, K_ij = Σ_{d in S_i} Q_j[d] J_d, S_i = the free-flyer
       // dofs (J = unit vectors in base coordinates: Q_j[ff0 + c]) and body i's chain; full mode: no Q (P = I).
-      const int kq = kp.full ? 0 : k;
+      // k is wave-uniform here (one sample per wave): scalar branches on it, not exec masks
+      const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);
+      const int jmax = 3 * nc - 1;  // the Q rows' loads are clamped into J_c's rows (finite, times zero K)
       for (int it = hl; it < nyi && valid; it += HW) {
         const int g = it / nbody, i = it - g * nbody + 1;
         const int r0 = g * nrows / kp.rg, r1 = (g + 1) * nrows / kp.rg;
@@ -1435,18 +1448,19 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         const double* bi = body + BODY_STRIDE * i;
         OutT* oi = out + 10 * (i - 1);
         auto g_row = [&](int r, double* G, int c0) {  // G[c0..5] of row r
-          const bool inS = (smask >> r) & 1ull;
+          // every load unconditional (J_w of any dof, Q rows clamped into J_c's finite rows)
+          const double sf = ((smask >> r) & 1ull) ? 1.0 : 0.0;
           const double* jr = Jws + 6 * r;
+          double qr[K1_QF_KMAX];
 #pragma unroll
-          for (int c = c0; c < 6; ++c) G[c] = inS ? jr[c] : 0.0;
+          for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = Jc[(j < jmax ? j : jmax) * nv + r];
 #pragma unroll
-          for (int j = 0; j < K1_QF_KMAX; ++j) {
-            if (j < kq) {
-              const double qr = Jc[j * nv + r];
+          for (int c = c0; c < 6; ++c) G[c] = sf * jr[c];
+          // all K1_QF_KMAX slots: K is zero past kq (branches here became per-FMA selects, 8 VALU per slot)
 #pragma unroll
-              for (int c = c0; c < 6; ++c) G[c] -= qr * Kq[j][c];
-            }
-          }
+          for (int j = 0; j < K1_QF_KMAX; ++j)
+#pragma unroll
+            for (int c = c0; c < 6; ++c) G[c] -= qr[j] * Kq[j][c];
         };
         {
           double FB[18];
@@ -1527,7 +1541,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         const int64_t pstep = (int64_t)NG * ldp;
         if constexpr (QF) {
           // P[r, bd + j] = δ - Σ_i Q_i[r] Q_i[bd + j]: the lane's two columns of Q in registers
-          const int kq = kp.full ? 0 : k;
+          const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);  // wave-uniform (one sample per wave)
           double qc[K1_QF_KMAX][2];
 #pragma unroll
           for (int j = 0; j < K1_QF_KMAX; ++j)
