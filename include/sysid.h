@@ -77,9 +77,10 @@ extern "C" {
 /* Rows of the Gram-only paths.  NULLSPACE: every sample contributes Zᵀ·A, the nv - rank(J_c) rows of its
  * system in an orthonormal basis Z of null(J_c) (ZᵀZ = P, so Σ (ZᵀA)ᵀ(ZᵀA) = Σ (PA)ᵀ(PA): the same Gram from
  * fewer rows; north_star's "batched QR/nullspace"; models with at most 4 contact frames).  PROJECTOR: the
- * reference's own P·A rows, nv per sample.  Neither flag: nullspace rows for the f64 Grams, whose MFMA
- * work they cut (Spot 20k f64 step -7%), and for f32 unless the model runs the Q-form K1 (G1); projector rows
- * for bf16, whose Gram is too cheap to repay the per-sample basis (measured in DESIGN.md). */
+ * reference's own P·A rows, nv per sample.  Neither flag: nullspace rows for the f64 / f32 Grams of models
+ * whose K1 is not the Q-form (Spot: step -7%, 10.4 of 18 rows), projector rows otherwise (G1: the Q-form K1
+ * costs far less than the basis saves) and for bf16, whose Gram is too cheap to repay the per-sample basis
+ * (measured in DESIGN.md). */
 #define SYSID_GRAM_PROJECTOR 64u
 #define SYSID_GRAM_NULLSPACE 128u
 

@@ -474,11 +474,12 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   const int prec = gram_prec(flags);
   // rows: nullspace (needs K1's register LU: at most K1_CMP_KMAX contact rows) or projector; by default the
   // nullspace rows for the f64 / f32 Grams and the projector rows for bf16 (include/sysid.h)
-  // auto: nullspace rows unless the projector rows come from the Q-form K1 (G1 125k f32 9.68 vs 10.28 ms, bf16
-  // 4.90 vs 5.99 ms) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save)
+  // auto: nullspace rows unless the projector rows come from the Q-form K1 (G1 125k f64 13.80 vs 14.95 ms, f32
+  // 7.81 vs 9.58, bf16 3.33 vs 5.23: its K1 is far cheaper than the nullspace K1 and G1 keeps 31 of 35 rows
+  // anyway) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save)
   const bool want_ns = (flags & SYSID_GRAM_NULLSPACE)   ? true
                        : (flags & SYSID_GRAM_PROJECTOR) ? false
-                                                        : prec == 0 || (prec == 1 && !e->k1m[1].qf);
+                                                        : prec != 2 && !e->k1m[prec].qf;
   const int cmp = want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
@@ -884,10 +885,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     if (st == hipSuccess) st = hipMemcpy(t, dealt[p].data(), dealt[p].size() * sizeof(int2), hipMemcpyHostToDevice);
   }
   // K1 shapes: per instantiation, the waves per workgroup that maximise resident waves per CU under the LDS
-  // budget.  Layout candidates of the projector rows: f64 (every stacked output) the plain layout (kept on ties)
-  // and the P overlay; f32 / bf16 chunk panels the Q-form when it applies (less arithmetic, no P slot; with f64
-  // elements its two column passes write each 80-byte body block in two pieces far apart in time, measured
-  // G1 125k K1 4.9 -> 7.2 ms, while bf16 gains 4.15 -> 3.38 ms).  The nullspace mode: CMP of the plain layout.
+  // budget.  Layout candidates of the projector rows: the Q-form when it applies (less arithmetic, no P slot),
+  // else the plain layout (kept on ties) and the P overlay.  The nullspace mode: CMP of the plain layout.
   auto shape = [&](sysid_engine::K1Shape& K, int prec, int cmp, const int* vars, const WLay* wls, const int* povs,
                    const int* qfs, int ncand) -> bool {
     int best = -1;
@@ -919,7 +918,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) {
     bool ok = true;
     for (int pr = 0; pr < 3 && ok; ++pr) {
-      if (pr > 0 && qf_ok) {
+      if (qf_ok) {
         const int vq[1] = {k1_qf_variant(v0)}, z[1] = {0}, one[1] = {1};
         ok = shape(e->k1m[pr], pr, 0, vq, &WLQ, z, one, 1);
       } else {

@@ -252,6 +252,13 @@ __device__ __forceinline__ double dpp_add(double v) {
   return v + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ __forceinline__ double pair_sum(double v) { return dpp_add<0xB1>(v); }  // quad_perm [1,0,3,2]
+// v of the partner lane (lane ^ 1)
+__device__ __forceinline__ double pair_swap(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0xB1, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
 // Sum over an aligned group of `lpr` lanes (1, 2, 4 or 8; uniform over the group): lane ^ 1, lane ^ 2,
 // then the half-row mirror (lane i <-> 7 - i pairs the two quads of an 8-lane group).
@@ -520,6 +527,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   double* Ms = wr + L.M;
   double* Ps = wr + L.P;
   double* H1 = wr + L.H1;
+  double* Qt = wr + L.Z;  // Q-form: Q transposed, K1_QF_KMAX entries per row (over W / Pt / pf)
   double* tps = wr + L.tp;
   double* dqs = wr + L.dqs;
 
@@ -606,12 +614,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   // issue priority: the column phase runs at 0, everything else at 2, so a wave in a latency-bound phase
   // issues first when its operands arrive (K1 -1 to -2%, Spot and G1)
   __builtin_amdgcn_s_setprio(2);
-  if constexpr (QF) {
-    // the Q-form's column phases read all K1_QF_KMAX row slots of J_c and multiply the ones past the sample's
-    // k by zero: rows not yet written must hold finite values (later samples leave finite rows behind)
-    for (int x = hl; x < 3 * nc * nv; x += HW) Jc[x] = 0.0;
-    wsync();
-  }
   const int hl_outer = hl;
   while (s < N) {
     // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
@@ -634,6 +636,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     double* Ms = wr + L.M;
     double* Ps = wr + L.P;
     double* H1 = wr + L.H1;
+    double* Qt = wr + L.Z;
     double* tps = wr + L.tp;
     double* dqs = wr + L.dqs;
     const double* q = wr + L.in;
@@ -1238,6 +1241,15 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
       const int r = e / 6, c = e - 6 * r;
       H1[e] = kp.has_ff ? Ps[r * nv + kp.ff0 + c] : 0.0;  // J_w[:, ff] = I (see h1_in_p)
     }
+    if constexpr (QF) {
+      // Qt[r][j] = Q_j[r] (zero past the sample's k rows; in the full mode P = I: no rows), over the dead
+      // W / Pt / contact-point slot: a row's K1_QF_KMAX entries are three 16-byte reads from one address
+      const int kq = kp.full ? 0 : k;
+      for (int e = hl; e < nv * K1_QF_KMAX; e += HW) {
+        const int r = e / K1_QF_KMAX, j = e - K1_QF_KMAX * r;
+        Qt[e] = j < kq ? Jc[j * nv + r] : 0.0;
+      }
+    }
     wsync();
     if (dbg != nullptr && s + half == 0)  // sysid_debug_lds: the LDS image of sample 0
       for (int x = hl; x < L.total; x += HW) dbg[x] = wr[x];
@@ -1407,93 +1419,102 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     } else if constexpr (QF) {
       // Q-form: G_i[r] = [r in S_i] J_r - Σ_j Q_j[r] K_ij, K_ij = Σ_{d in S_i} Q_j[d] J_d, S_i = the free-flyer
       // dofs (J = unit vectors in base coordinates: Q_j[ff0 + c]) and body i's chain; full mode: no Q (P = I).
-      // k is wave-uniform here (one sample per wave): scalar branches on it, not exec masks
+      // Lane = (body i, block half h), every row: h = 0 the mass / first-moment columns 0..3, h = 1 the inertia
+      // columns 4..9, both as one 6 x 6 matrix F6 (zero-padded) times G, so the two lanes of a body run the same
+      // code and write their 32 + 48 bytes of the row's 80-byte block with the same store instructions (lanes
+      // 2m, 2m + 1: a row of the panel per store set).  The pair shares G: lane h forms components 3h..3h+2
+      // (its three columns of K) and takes the other three from its partner by DPP; F6's columns are permuted
+      // per lane to [own three | partner's three].  k is wave-uniform (one sample per wave): the row loop is
+      // specialised for k <= 3 and k <= 6.
       const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);
-      const int jmax = 3 * nc - 1;  // the Q rows' loads are clamped into J_c's rows (finite, times zero K)
-      for (int it = hl; it < nyi && valid; it += HW) {
-        const int g = it / nbody, i = it - g * nbody + 1;
-        const int r0 = g * nrows / kp.rg, r1 = (g + 1) * nrows / kp.rg;
-        // K first (F is not live yet), walking the chain in a rolled loop: unrolled over the chain slots the
-        // compiler kept every slot's loads in flight (~350 registers)
+      const int nyh = 2 * nbody;  // even: both lanes of a pair are always active together
+      for (int it = hl; it < nyh && valid; it += HW) {
+        const int i = (it >> 1) + 1, h = it & 1, c3 = 3 * h;
+        // K (this lane's three columns) first, F is not live yet; the chain in a rolled loop
         const int cl = chain_len[i];
         unsigned long long smask = kp.has_ff ? (0x3Full << kp.ff0) : 0ull;
-        double Kq[K1_QF_KMAX][6];
+        // Qt is zero past the sample's k rows, so every slot runs unconditionally
+        double Kq[K1_QF_KMAX][3];
+        const int ffo = kp.has_ff ? kp.ff0 : 0;
+        const double fff = kp.has_ff ? 1.0 : 0.0;
 #pragma unroll
-        for (int j = 0; j < K1_QF_KMAX; ++j)
+        for (int c = 0; c < 3; ++c) {
+          const double* qf = Qt + (ffo + c3 + c) * K1_QF_KMAX;
 #pragma unroll
-          for (int c = 0; c < 6; ++c) Kq[j][c] = j < kq && kp.has_ff ? Jc[j * nv + kp.ff0 + c] : 0.0;
+          for (int j = 0; j < K1_QF_KMAX; ++j) Kq[j][c] = fff * qf[j];
+        }
 #pragma unroll 1
         for (int t = 0; t < cl; ++t) {
           const int d = chain[i * kp.maxch + t];
           smask |= 1ull << d;
-          const double2* jw = reinterpret_cast<const double2*>(Jws + 6 * d);
-          double a6[6];
+          const double* jw = Jws + 6 * d + c3;
+          const double* qd = Qt + d * K1_QF_KMAX;
+          double a3[3];
 #pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const double2 v = jw[c];
-            a6[2 * c] = v.x;
-            a6[2 * c + 1] = v.y;
-          }
+          for (int c = 0; c < 3; ++c) a3[c] = jw[c];
 #pragma unroll
           for (int j = 0; j < K1_QF_KMAX; ++j) {
-            if (j < kq) {
-              const double qv = Jc[j * nv + d];
+            const double qv = qd[j];
 #pragma unroll
-              for (int c = 0; c < 6; ++c) Kq[j][c] += qv * a6[c];
-            }
+            for (int c = 0; c < 3; ++c) Kq[j][c] += qv * a3[c];
           }
         }
-        // two passes over the rows, one per half of the body block (registers: K + half a block): the
-        // inertia columns 4..9 (angular part of G only), then the mass / first-moment columns 0..3
+        // F6[c] . [own G | partner's G] = output c of this lane's half
         const double* bi = body + BODY_STRIDE * i;
-        OutT* oi = out + 10 * (i - 1);
-        auto g_row = [&](int r, double* G, int c0) {  // G[c0..5] of row r
-          // every load unconditional (J_w of any dof, Q rows clamped into J_c's finite rows)
-          const double sf = ((smask >> r) & 1ull) ? 1.0 : 0.0;
-          const double* jr = Jws + 6 * r;
-          double qr[K1_QF_KMAX];
-#pragma unroll
-          for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = Jc[(j < jmax ? j : jmax) * nv + r];
-#pragma unroll
-          for (int c = c0; c < 6; ++c) G[c] = sf * jr[c];
-          // all K1_QF_KMAX slots: K is zero past kq (branches here became per-FMA selects, 8 VALU per slot)
-#pragma unroll
-          for (int j = 0; j < K1_QF_KMAX; ++j)
-#pragma unroll
-            for (int c = c0; c < 6; ++c) G[c] -= qr[j] * Kq[j][c];
-        };
+        double F6[6][6];
         {
-          double FB[18];
-          body_block_inertia(bi, FB);
+          double FA[24], FB[18];
+          if (h == 0) body_block_mass(bi, FA);
+          else body_block_inertia(bi, FB);
+#pragma unroll
+          for (int c = 0; c < 6; ++c)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+              const int qb = (q + 3) % 6;  // the G component in slot q of an h = 1 lane (compile-time indices)
+              F6[c][q] = h == 0 ? (c < 4 ? FA[6 * c + q] : 0.0) : (qb < 3 ? 0.0 : FB[3 * c + qb - 3]);
+            }
+        }
+        OutT* oi = out + 10 * (i - 1) + 4 * h;
+        const double* jrs = Jws + c3;
+        auto rows = [&](auto kqc) {
+          constexpr int KQ = decltype(kqc)::value;
 #pragma unroll 1
-          for (int r = r0; r < r1; ++r) {
+          for (int r = 0; r < nrows; ++r) {
+            const double sf = ((smask >> r) & 1ull) ? 1.0 : 0.0;
+            const double* jr = jrs + 6 * r;
+            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
+            double qr[K1_QF_KMAX];
+#pragma unroll
+            for (int j = 0; j < (KQ + 1) / 2; ++j) {
+              const double2 v = q2[j];
+              qr[2 * j] = v.x;
+              qr[2 * j + 1] = v.y;
+            }
             double G[6];
-            g_row(r, G, 3);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) G[c] = sf * jr[c];
+#pragma unroll
+            for (int j = 0; j < KQ; ++j)
+#pragma unroll
+              for (int c = 0; c < 3; ++c) G[c] -= qr[j] * Kq[j][c];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) G[3 + c] = pair_swap(G[c]);
             double y[6];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) y[c] = G[3] * FB[3 * c] + G[4] * FB[3 * c + 1] + G[5] * FB[3 * c + 2];
-            OutT* o2 = oi + (int64_t)r * ldp + 4;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) panel_store(o2 + 2 * c, y[2 * c], y[2 * c + 1]);
-          }
-        }
-        {
-          double FA[24];
-          body_block_mass(bi, FA);
-#pragma unroll 1
-          for (int r = r0; r < r1; ++r) {
-            double G[6];
-            g_row(r, G, 0);
-            double y[4];
-#pragma unroll
             for (int c = 0; c < 4; ++c)
-              y[c] = G[0] * FA[6 * c] + G[1] * FA[6 * c + 1] + G[2] * FA[6 * c + 2] + G[3] * FA[6 * c + 3] +
-                     G[4] * FA[6 * c + 4] + G[5] * FA[6 * c + 5];
+              y[c] = G[0] * F6[c][0] + G[1] * F6[c][1] + G[2] * F6[c][2] + G[3] * F6[c][3] + G[4] * F6[c][4] +
+                     G[5] * F6[c][5];
+            // outputs 4, 5 are stored by h = 1 lanes only, whose slots 3..5 (the partner's components) are zero
+#pragma unroll
+            for (int c = 4; c < 6; ++c) y[c] = G[0] * F6[c][0] + G[1] * F6[c][1] + G[2] * F6[c][2];
             OutT* o2 = oi + (int64_t)r * ldp;
             panel_store(o2, y[0], y[1]);
             panel_store(o2 + 2, y[2], y[3]);
+            if (h) panel_store(o2 + 4, y[4], y[5]);
           }
-        }
+        };
+        if (kq <= 3) rows(std::integral_constant<int, 3>{});
+        else rows(std::integral_constant<int, K1_QF_KMAX>{});
       }
     } else {
       for (int it = hl; it < nyi && valid; it += HW) {
@@ -1542,20 +1563,20 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
         if constexpr (QF) {
           // P[r, bd + j] = δ - Σ_i Q_i[r] Q_i[bd + j]: the lane's two columns of Q in registers
           const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);  // wave-uniform (one sample per wave)
+          (void)kq;
           double qc[K1_QF_KMAX][2];
 #pragma unroll
           for (int j = 0; j < K1_QF_KMAX; ++j)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) qc[j][u] = j < kq ? Jc[j * nv + bd + jc[u]] : 0.0;
+            for (int u = 0; u < 2; ++u) qc[j][u] = Qt[(bd + jc[u]) * K1_QF_KMAX + j];  // zero past k
           for (int r = fg; r < nrows; r += NG, po += pstep) {
             double pe[2] = {r == bd + jc[0] ? 1.0 : 0.0, r == bd + jc[1] ? 1.0 : 0.0};
+            const double* qrow = Qt + r * K1_QF_KMAX;
 #pragma unroll
             for (int j = 0; j < K1_QF_KMAX; ++j) {
-              if (j < kq) {
-                const double qr = Jc[j * nv + r];
-                pe[0] -= qr * qc[j][0];
-                pe[1] -= qr * qc[j][1];
-              }
+              const double qr = qrow[j];
+              pe[0] -= qr * qc[j][0];
+              pe[1] -= qr * qc[j][1];
             }
             const double t = tps[r];
             double v2[2];

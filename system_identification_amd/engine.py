@@ -353,7 +353,7 @@ class Engine:
         """Normal equations of N samples without materialising the N·nv-row panel (stream-ordered).
         precision: "f64" (parity), "f32" or "bf16" (MFMA in reduced precision, error reported).
         rows: "nullspace" (each sample's nv - rank(J_c) rows Zᵀ·A, ZᵀZ = P), "projector" (the reference's nv
-        rows P·A) or "auto" (nullspace for f64, and for f32 unless the Q-form K1 applies; projector for bf16); all give Σ AᵀPA."""
+        rows P·A) or "auto" (nullspace for f64 / f32 unless the model runs the Q-form K1; projector otherwise and for bf16); all give Σ AᵀPA."""
         import torch
         self._check_inputs(d_in, N)
         self._check_buffer(bufs["gram"], "gram", torch.float64, self.panel_cols * self.panel_cols)
