@@ -147,6 +147,8 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
 size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N);
 int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
                                 double* d_gram, void* d_workspace, size_t workspace_bytes, void* stream);
+/* The rows sysid_build_gram_device uses for these flags: 1 = nullspace (Zᵀ·A), 0 = projector (P·A), < 0 error. */
+int32_t sysid_gram_rows(const sysid_engine* e, uint32_t flags);
 
 /* Torque-prediction errors: print_tau_prediction_rmse
  * (src/sys_identification.py:421-437) as one reduction over the stacked panel instead of a second

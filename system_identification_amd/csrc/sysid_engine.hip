@@ -468,19 +468,23 @@ size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every pr
 // ev (optional, diagnostics): 2 events per chunk + 2 for K3, recorded around each K1 (+ row list) / K2 / K3 launch.
 // Nullspace mode: K1 emits Zᵀ·A, nv - rank(J_c) rows per sample, k1s_seg_sums / k1s_row_list list them and K2
 // gathers them; projector mode: the reference's P·A rows (nv per sample), contiguous.
+// The Gram-only rows for these flags: 1 = nullspace (needs K1's register LU: at most K1_CMP_KMAX contact rows),
+// 0 = projector.  Neither flag: nullspace rows unless the projector rows come from the Q-form K1 (G1 125k f64
+// 13.80 vs 14.95 ms, f32 7.81 vs 9.58, bf16 3.33 vs 5.23: its K1 is far cheaper than the nullspace K1, and G1 keeps
+// 31 of 35 rows anyway) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save).
+int gram_nullspace(const sysid_engine* e, uint32_t flags) {
+  const int prec = gram_prec(flags);
+  const bool want_ns = (flags & SYSID_GRAM_NULLSPACE)   ? true
+                       : (flags & SYSID_GRAM_PROJECTOR) ? false
+                                                        : prec != 2 && !e->k1m[prec].qf;
+  return want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
+}
+
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
-  // rows: nullspace (needs K1's register LU: at most K1_CMP_KMAX contact rows) or projector; by default the
-  // nullspace rows for the f64 / f32 Grams and the projector rows for bf16 (include/sysid.h)
-  // auto: nullspace rows unless the projector rows come from the Q-form K1 (G1 125k f64 13.80 vs 14.95 ms, f32
-  // 7.81 vs 9.58, bf16 3.33 vs 5.23: its K1 is far cheaper than the nullspace K1 and G1 keeps 31 of 35 rows
-  // anyway) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save)
-  const bool want_ns = (flags & SYSID_GRAM_NULLSPACE)   ? true
-                       : (flags & SYSID_GRAM_PROJECTOR) ? false
-                                                        : prec != 2 && !e->k1m[prec].qf;
-  const int cmp = want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
+  const int cmp = gram_nullspace(e, flags);
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
                    gram_ws_bytes_prec(e, N, prec));
@@ -1348,6 +1352,11 @@ int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, cons
   (void)hipFree(e->d_dump);
   e->d_dump = nullptr;
   return rc;
+}
+
+int32_t sysid_gram_rows(const sysid_engine* e, uint32_t flags) {
+  if (!e) return SYSID_E_INVALID;
+  return gram_nullspace(e, flags);
 }
 
 int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4) {

@@ -55,6 +55,7 @@ SIGNATURES = [
     ("sysid_debug_lds", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _c.c_int64]),
     ("sysid_debug_layout", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_debug_k1_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
+    ("sysid_gram_rows", _c.c_int32, [_vp, _c.c_uint32]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
@@ -367,6 +368,12 @@ class Engine:
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)
+
+    def gram_rows(self, precision: str = "f64", rows: str = "auto") -> str:
+        """The rows build_gram_device uses: "nullspace" (Zᵀ·A) or "projector" (P·A)."""
+        rc = self.lib.sysid_gram_rows(self._h, GRAM_PRECISION[precision] | GRAM_ROWS[rows])
+        self._check(min(rc, 0))
+        return "nullspace" if rc == 1 else "projector"
 
     def k1_config(self) -> list:
         """K1 launch shape of the f64 panel [waves per workgroup, workgroups per CU, LDS bytes, chain slots]."""
