@@ -56,6 +56,9 @@ def parse():
                     help="threads of the extra multi-core C oracle timing (0 = off; 16 = the GPU box's CPU share)")
     ap.add_argument("--ref-samples", type=int, default=2000,
                     help="samples of the numpy reference-structure CPU leg (0 = off)")
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="untimed steps run back to back for at least this long before the warmup steps, so the "
+                         "GPU's clocks reach their operating point (0 = off); reported as `settle` in the JSON")
     return ap.parse_args()
 
 
@@ -236,13 +239,15 @@ def main():
             launch(torch.cuda.current_stream(local).cuda_stream)
         graph_used = True
 
-        def step():
+        def compute():
             g.replay()
-            exchange()
     else:
-        def step():
+        def compute():
             launch(stream.cuda_stream)
-            exchange()
+
+    def step():
+        compute()
+        exchange()
 
     # The host-entry-point legs (their own measurement, SURVEY §8d's end-to-end rate; PCIe-inclusive, never the
     # headline value) run here, before the warmup steps: ~40 ms of GPU work that brings the clocks to their
@@ -253,6 +258,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = e2e_legs(eng, data, N)
         torch.cuda.synchronize()
+    # Clock settle (untimed, every rank): steps back to back until --settle-ms of wall time has passed.  The
+    # driver's 5 warmup steps are ~2 ms of Spot work; the clocks take longer than that to ramp (step_times of a
+    # 20-step run after 5 warmup steps: first-quartile mean 0.406 ms, last 0.353, steady state 0.318,
+    # profiles/r03_j).  Same launches as the timed steps minus the exchange (ranks may settle for different step
+    # counts, so no collective runs here); what is timed does not change.
+    settle_steps, t_settle = 0, time.perf_counter()
+    while args.settle_ms > 0 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            compute()
+        settle_steps += 8
+        torch.cuda.synchronize()
+    settle = {"steps": settle_steps, "ms": round((time.perf_counter() - t_settle) * 1e3, 1)}
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -295,6 +312,14 @@ def main():
         # nv-row count stays in K2_TFps / gram_gflops
         rows_per_sample = float(np.mean(nv - 3 * (data["contact"] != 0).sum(axis=0)))
     k2_exec_tfs = k2_tfs * rows_per_sample / nv
+    k2cfg = eng.k2_config()
+    structured = not args.gram_only and k2cfg[1] > 0
+    if structured:
+        # the structured f64 Gram (sysid_kernels.h K2Struct): the MFMA tiles cover the first 16·ntm columns, the
+        # B_c / tau_proj columns past them are VALU sums over the joint rows; roofline.achieved counts the MFMA
+        # SYRK it executes, K2_TFps / gram_gflops stay on §8(d)'s dense count
+        cm = 16 * k2cfg[1]
+        k2_exec_tfs = n_time * nv * cm * (cm + 1) / (ms[1] * 1e-3) / 1e12
     if ms[0] >= ms[1]:
         traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N) if not args.gram_only else (None, None)
         roof = {"kernel": "k1_regressor_panel", "bound": "hbm", "achieved": round(k1_gbs, 1),
@@ -307,7 +332,10 @@ def main():
         roof = {"kernel": "k2_gram_syrk", "bound": "mfma", "achieved": round(k2_exec_tfs, 3),
                 "peak": peak, "unit": "TFLOP/s", "frac": round(k2_exec_tfs / peak, 4),
                 "traffic": traffic, "traffic_source": src,
-                "algorithmic_flops_per_launch": round(n_time * flops_k2 * rows_per_sample / nv),
+                "algorithmic_flops_per_launch": round(n_time * nv * (16 * k2cfg[1]) * (16 * k2cfg[1] + 1)) if structured
+                else round(n_time * flops_k2 * rows_per_sample / nv),
+                "structured_gram": ({"mfma_columns": 16 * k2cfg[1], "valu_columns": f"{16 * k2cfg[1]}..{W}"}
+                                    if structured else None),
                 "rows_per_sample": round(rows_per_sample, 3), "avg_launch_ms": round(ms[1], 5)}
 
     ms_step = elapsed / args.steps * 1e3
@@ -342,6 +370,7 @@ def main():
                    "timed_region": ("K1 + K2 per panel chunk + K3 (Gram-only)" if args.gram_only else "K1 + K2 + K3")
                    + ", HBM-resident inputs and outputs" + (", + the Gram all-reduce" if world > 1 else "")},
         "step_times": step_stats,
+        "settle": settle,
         "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
         "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},

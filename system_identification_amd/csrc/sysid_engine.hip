@@ -18,6 +18,7 @@
 
 #include "sysid.h"
 #include "sysid_kernels.h"
+#include "sysid_launch.h"
 
 using namespace sysid_dev;
 
@@ -65,6 +66,10 @@ struct sysid_engine {
     int blk = 0;  // the register-blocked kernel (k2_gram_syrk_blk / _bf16_blk): one workgroup per CU
     int2* d_tiles = nullptr;  // [super slots | tile slots]
   } k2d[3];
+  // structured f64 Gram (k2_gram_syrk NVS = 18: B_c / tau tile columns on the VALU, sysid_kernels.h K2Struct):
+  // its own deal of the MFMA tile columns [0, k2s_ntm) plus the structured tiles (k2s.ngroups == 0: not used)
+  Deal k2s;
+  int k2s_ntm = 0, k2s_slot0 = 0;
   // host-API buffers (grow-only)
   double* d_in = nullptr;
   size_t in_cap = 0;
@@ -111,7 +116,8 @@ int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
 }
 
 size_t slab_bytes(const sysid_engine* e, int64_t rows, int prec = 0) {
-  return align256((size_t)ksplit_for(e, rows, prec) * e->k2d[prec].nslots * 256 * sizeof(double));
+  const int nslots = std::max(e->k2d[prec].nslots, prec == 0 ? e->k2s.nslots : 0);  // either f64 deal
+  return align256((size_t)ksplit_for(e, rows, prec) * nslots * 256 * sizeof(double));
 }
 
 int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
@@ -124,15 +130,18 @@ int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
   return SYSID_OK;
 }
 
-// K1 instantiations: chain slots x compile-time nv x samples per wave.  Quadrupeds (nv = 18) run two
-// samples per wave; anything else one, with nv read at run time (a compile-time nv = 35 for the humanoid
-// ran 1.8x slower, its unrolled serial phases being heavier than the saved address arithmetic).
-constexpr int SYSID_K1_SPW_QUAD = 2, SYSID_K1_SPW_GEN = 1;
-// Chain slots of the nv = 18 kernel: the quadrupeds' legs are 3 revolute joints deep (3 measured 2% faster
-// than 4 on Spot: no dead slot in the column phase).
-constexpr int SYSID_K1_QCH = 3;
-// ...P: the P-overlay layout (wave_layout pov); ...Q: the Q-form (at most K1_QF_KMAX contact rows, no P)
-enum { K1_C4_NV18, K1_C4, K1_C12, K1_C16, K1_C12P, K1_C16P, K1_C4Q, K1_C12Q, K1_C16Q };
+// K1 variants and their instantiations: sysid_launch.h / sysid_k1_inst.hip.
+using sysid_launch::K1_C4_NV18;
+using sysid_launch::K1_C4;
+using sysid_launch::K1_C12;
+using sysid_launch::K1_C16;
+using sysid_launch::K1_C12P;
+using sysid_launch::K1_C16P;
+using sysid_launch::K1_C4Q;
+using sysid_launch::K1_C12Q;
+using sysid_launch::K1_C16Q;
+constexpr int SYSID_K1_SPW_QUAD = sysid_launch::SPW_QUAD, SYSID_K1_SPW_GEN = sysid_launch::SPW_GEN;
+constexpr int SYSID_K1_QCH = sysid_launch::QCH;
 int k1_qf_variant(int variant) {
   return variant == K1_C4 ? K1_C4Q : variant == K1_C12 ? K1_C12Q : variant == K1_C16 ? K1_C16Q : -1;
 }
@@ -154,23 +163,17 @@ int k1_spw(int variant) { return variant == K1_C4_NV18 ? SYSID_K1_SPW_QUAD : SYS
 // wave_layout's `hw`: lanes per sample of the compile-time-nv kernel (P over Z), 0 for the others.
 int k1_layout_hw(int variant) { return variant == K1_C4_NV18 ? 64 / k1_spw(variant) : 0; }
 
-// The instantiation of a variant for a panel element type (prec: 0 f64, 1 f32, 2 bf16).
-template <typename OutT>
-const void* k1_fn_t(int variant) {
-  switch (variant) {
-    case K1_C4_NV18: return reinterpret_cast<const void*>(k1_regressor_panel<SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, OutT>);
-    case K1_C4: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT>);
-    case K1_C12: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT>);
-    case K1_C12P: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 1>);
-    case K1_C16P: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 1>);
-    case K1_C4Q: return reinterpret_cast<const void*>(k1_regressor_panel<4, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>);
-    case K1_C12Q: return reinterpret_cast<const void*>(k1_regressor_panel<12, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>);
-    case K1_C16Q: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>);
-    default: return reinterpret_cast<const void*>(k1_regressor_panel<16, 0, SYSID_K1_SPW_GEN, OutT>);
-  }
-}
+// The kernel of a variant for a panel element type (prec: 0 f64, 1 f32, 2 bf16), for occupancy queries.
 const void* k1_fn(int variant, int prec = 0) {
-  return prec == 0 ? k1_fn_t<double>(variant) : prec == 1 ? k1_fn_t<float>(variant) : k1_fn_t<__bf16>(variant);
+  return prec == 0 ? sysid_launch::k1_fn<0, 0>(variant)
+         : prec == 1 ? sysid_launch::k1_fn<1, 0>(variant)
+                     : sysid_launch::k1_fn<2, 0>(variant);
+}
+// The nullspace-mode instantiation of a variant (OutT of the Gram arithmetic).
+const void* k1_fn_cmp(int variant, int prec) {
+  return prec == 0 ? sysid_launch::k1_fn<0, 1>(variant)
+         : prec == 1 ? sysid_launch::k1_fn<1, 1>(variant)
+                     : sysid_launch::k1_fn<2, 1>(variant);
 }
 
 // Panel element of each Gram arithmetic: 0 = f64 (parity; every stacked output), 1 = f32, 2 = bf16 (the
@@ -179,56 +182,6 @@ size_t prec_bytes(int prec) { return prec == 0 ? 8 : prec == 1 ? 4 : 2; }
 
 // Gram arithmetic selected by the flags: 0 = f64 (parity), 1 = f32 MFMA, 2 = bf16 MFMA (error reported).
 int gram_prec(uint32_t flags) { return (flags & SYSID_GRAM_BF16) ? 2 : (flags & SYSID_GRAM_F32) ? 1 : 0; }
-
-template <typename OutT, int CMP = 0>
-void k1_launch_typed(sysid_engine* e, int variant, dim3 g1, dim3 b1, size_t lds, hipStream_t st, const K1Params& kp,
-                     const double* d_in, int64_t N, int64_t ld, OutT* d_panel, int64_t ld_panel,
-                     unsigned long long* work, double* dbg, int* rcount) {
-#define SYSID_K1_LAUNCH(MAXCH, NVC, SPW, POV)                                                                      \
-  hipLaunchKernelGGL((k1_regressor_panel<MAXCH, NVC, SPW, OutT, POV, CMP>), g1, b1, lds, st, kp, e->d_mimg, d_in, N, \
-                     ld, d_panel, ld_panel, work, dbg, rcount)
-#define SYSID_K1_LAUNCH_Q(MAXCH)                                                                                   \
-  hipLaunchKernelGGL((k1_regressor_panel<MAXCH, 0, SYSID_K1_SPW_GEN, OutT, 0, 0, 1>), g1, b1, lds, st, kp,         \
-                     e->d_mimg, d_in, N, ld, d_panel, ld_panel, work, dbg, rcount)
-  switch (variant) {
-    case K1_C4_NV18: SYSID_K1_LAUNCH(SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD, 0); break;
-    case K1_C4: SYSID_K1_LAUNCH(4, 0, SYSID_K1_SPW_GEN, 0); break;
-    case K1_C12: SYSID_K1_LAUNCH(12, 0, SYSID_K1_SPW_GEN, 0); break;
-    case K1_C16: SYSID_K1_LAUNCH(16, 0, SYSID_K1_SPW_GEN, 0); break;
-    case K1_C12P:
-      if constexpr (!CMP) SYSID_K1_LAUNCH(12, 0, SYSID_K1_SPW_GEN, 1);
-      break;
-    case K1_C16P:
-      if constexpr (!CMP) SYSID_K1_LAUNCH(16, 0, SYSID_K1_SPW_GEN, 1);
-      break;
-    case K1_C4Q:
-      if constexpr (!CMP) SYSID_K1_LAUNCH_Q(4);
-      break;
-    case K1_C12Q:
-      if constexpr (!CMP) SYSID_K1_LAUNCH_Q(12);
-      break;
-    case K1_C16Q:
-      if constexpr (!CMP) SYSID_K1_LAUNCH_Q(16);
-      break;
-  }
-#undef SYSID_K1_LAUNCH
-#undef SYSID_K1_LAUNCH_Q
-}
-
-// The nullspace-mode instantiation of a variant (OutT of the Gram arithmetic), for the occupancy query.
-const void* k1_fn_cmp(int variant, int prec) {
-#define SYSID_K1_FN(MAXCH, NVC, SPW)                                                                              \
-  (prec == 0   ? reinterpret_cast<const void*>(k1_regressor_panel<MAXCH, NVC, SPW, double, 0, 1>)                \
-   : prec == 1 ? reinterpret_cast<const void*>(k1_regressor_panel<MAXCH, NVC, SPW, float, 0, 1>)                 \
-               : reinterpret_cast<const void*>(k1_regressor_panel<MAXCH, NVC, SPW, __bf16, 0, 1>))
-  switch (variant) {
-    case K1_C4_NV18: return SYSID_K1_FN(SYSID_K1_QCH, 18, SYSID_K1_SPW_QUAD);
-    case K1_C4: return SYSID_K1_FN(4, 0, SYSID_K1_SPW_GEN);
-    case K1_C12: return SYSID_K1_FN(12, 0, SYSID_K1_SPW_GEN);
-    default: return SYSID_K1_FN(16, 0, SYSID_K1_SPW_GEN);
-  }
-#undef SYSID_K1_FN
-}
 
 // cmp: the Gram-only nullspace mode (rcount: its per-sample row counts).
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
@@ -252,126 +205,42 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
   const int64_t cap = (int64_t)e->cus * bpc;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + waves - 1) / waves));
   const dim3 g1((unsigned)grid), b1(64 * waves);
-#define SYSID_K1_TYPED(CMPV)                                                                                       \
-  if (prec == 0)                                                                                                   \
-    k1_launch_typed<double, CMPV>(e, variant, g1, b1, lds, st, kp, d_in, N, ld, static_cast<double*>(d_panel),     \
-                                  ld_panel, work, dbg, rcount);                                              \
-  else if (prec == 1)                                                                                              \
-    k1_launch_typed<float, CMPV>(e, variant, g1, b1, lds, st, kp, d_in, N, ld, static_cast<float*>(d_panel),       \
-                                 ld_panel, work, dbg, rcount);                                               \
-  else                                                                                                             \
-    k1_launch_typed<__bf16, CMPV>(e, variant, g1, b1, lds, st, kp, d_in, N, ld, static_cast<__bf16*>(d_panel),     \
-                                  ld_panel, work, dbg, rcount);
-  if (cmp) {
-    SYSID_K1_TYPED(1)
-  } else {
-    SYSID_K1_TYPED(0)
-  }
-#undef SYSID_K1_TYPED
+  // the instantiation unit of (panel type, row mode)
+  using K1L = void (*)(int, dim3, dim3, size_t, hipStream_t, const K1Params&, const uint32_t*, const double*, int64_t,
+                       int64_t, void*, int64_t, unsigned long long*, double*, int*);
+  static constexpr K1L k1l[6] = {sysid_launch::k1_launch<0, 0>, sysid_launch::k1_launch<0, 1>,
+                                 sysid_launch::k1_launch<1, 0>, sysid_launch::k1_launch<1, 1>,
+                                 sysid_launch::k1_launch<2, 0>, sysid_launch::k1_launch<2, 1>};
+  k1l[prec * 2 + (cmp ? 1 : 0)](variant, g1, b1, lds, st, kp, e->d_mimg, d_in, N, ld, d_panel, ld_panel, work, dbg,
+                                rcount);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
 
 // rowlist / d_rows: the nullspace mode's gathered rows (k1s_row_list; `rows` is then only the bound the split
-// was sized for): the LDS-DMA kernels for every width and arithmetic.
+// was sized for): the LDS-DMA / blocked kernels for every width and arithmetic (sysid_k2_inst.hip).
+// sx: the structured f64 Gram (sx.in != nullptr; the engine's k2s deal), else the arithmetic's own deal.
 int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
-              double* slab, hipStream_t st, int prec, const int* rowlist = nullptr, const int* d_rows = nullptr) {
+              double* slab, hipStream_t st, int prec, const int* rowlist = nullptr, const int* d_rows = nullptr,
+              const K2Struct& sx = K2Struct{}) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
-  const sysid_engine::Deal& D = e->k2d[prec];
-  const dim3 g2(D.ngroups * ks), b2(64 * k2_waves(e->ntc));
-  const double* p64 = static_cast<const double*>(d_panel);
-  const float* p32 = static_cast<const float*>(d_panel);
-  const __bf16* p16 = static_cast<const __bf16*>(d_panel);
-  const bool gather = rowlist != nullptr;
-  switch (e->ntc) {
-// f64 / f32 Gram kernels: LDS-DMA staged (three buffers) for wide Grams, register-staged for narrow ones
-// (measured, 20k samples: G1 K2 1.81 -> 1.66 ms with the DMA kernel; Spot 0.202 -> 0.213 ms, so not there);
-// the gathered rows of the nullspace mode always go through the DMA kernels.
-#define SYSID_K2_DMA_LAUNCH(T, P, NTC, KC)                                                                          \
-  if (gather)                                                                                                       \
-    hipLaunchKernelGGL((k2_gram_syrk_dma<T, NTC, KC, true>), g2, b2, 0, st, P, rows, ld_panel, D.d_tiles,         \
-                       D.ngroups, ks, D.nslots, accumulate, slab, rowlist, d_rows);                                 \
-  else                                                                                                              \
-    hipLaunchKernelGGL((k2_gram_syrk_dma<T, NTC, KC>), g2, b2, 0, st, P, rows, ld_panel, D.d_tiles, D.ngroups,    \
-                       ks, D.nslots, accumulate, slab, nullptr, nullptr);
-#define SYSID_K2_BLK(T, P, NTC)                                                                                    \
-  if (gather)                                                                                                       \
-    hipLaunchKernelGGL((k2_gram_syrk_blk<T, NTC, true>), g2, dim3(512), 0, st, P, rows, ld_panel, ks, D.nslots,     \
-                       accumulate, slab, rowlist, d_rows);                                                          \
-  else                                                                                                              \
-    hipLaunchKernelGGL((k2_gram_syrk_blk<T, NTC>), g2, dim3(512), 0, st, P, rows, ld_panel, ks, D.nslots,           \
-                       accumulate, slab, nullptr, nullptr);
-#define SYSID_K2_F64(NTC, KC)                                                                                      \
-  if constexpr (k2b_supported(NTC)) {                                                                               \
-    SYSID_K2_BLK(double, p64, NTC)                                                                                  \
-  } else if constexpr (NTC >= 16) {                                \
-    SYSID_K2_DMA_LAUNCH(double, p64, NTC, k2_dma_kc(NTC))                                                           \
-  } else if (gather) {                                                                                              \
-    hipLaunchKernelGGL((k2_gram_syrk_dma<double, NTC, k2_dma_kc(NTC), true>), g2, b2, 0, st, p64, rows, ld_panel,  \
-                       D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist, d_rows);                      \
-  } else {                                                                                                          \
-    hipLaunchKernelGGL((k2_gram_syrk<double, NTC, KC>), g2, b2, 0, st, p64, rows, ld_panel, D.d_tiles,             \
-                       D.ngroups, ks, D.nslots, accumulate, slab);                                                  \
-  }
-#define SYSID_K2_F32(NTC, KC) /* f32: twice the rows of the f64 chunk in the same LDS bytes */                        \
-  if constexpr (k2b_supported(NTC)) {                                                                               \
-    SYSID_K2_BLK(float, p32, NTC)                                                                                   \
-  } else if constexpr (NTC >= 16) {                                \
-    SYSID_K2_DMA_LAUNCH(float, p32, NTC, 2 * k2_dma_kc(NTC))                                                        \
-  } else if (gather) {                                                                                              \
-    hipLaunchKernelGGL((k2_gram_syrk_dma<float, NTC, 2 * k2_dma_kc(NTC), true>), g2, b2, 0, st, p32, rows,         \
-                       ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist, d_rows);            \
-  } else {                                                                                                          \
-    hipLaunchKernelGGL((k2_gram_syrk<float, NTC, 2 * KC>), g2, b2, 0, st, p32, rows, ld_panel, D.d_tiles,          \
-                       D.ngroups, ks, D.nslots, accumulate, slab);                                                  \
-  }
-#define SYSID_K2_CASE(NTC, KC)                                                                                     \
-  case NTC:                                                                                                       \
-    if (prec == 0) {                                                                                              \
-      SYSID_K2_F64(NTC, KC)                                                                                       \
-    } else if (prec == 1) {                                                                                       \
-      SYSID_K2_F32(NTC, KC)                                                                                       \
-    } else if constexpr (k2b_supported(NTC)) {                                                                    \
-      if (gather)                                                                                                 \
-        hipLaunchKernelGGL((k2_gram_syrk_bf16_blk<NTC, true>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16, rows,    \
-                           ld_panel, ks, D.nslots, accumulate, slab, rowlist, d_rows);                            \
-      else                                                                                                        \
-        hipLaunchKernelGGL((k2_gram_syrk_bf16_blk<NTC>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16, rows,          \
-                           ld_panel, ks, D.nslots, accumulate, slab, nullptr, nullptr);                           \
-    } else if (gather) {                                                                                          \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC), true>), g2, dim3(64 * K2_BF16_WAVES), 0, \
-                         st, p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, rowlist,  \
-                         d_rows);                                                                                 \
-    } else if constexpr (NTC >= 16) {                                                                            \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16_tr<NTC, k2_bf16_tr_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st,    \
-                         p16, rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab, nullptr,      \
-                         nullptr);                                                                                \
-    } else {                                                                                                      \
-      hipLaunchKernelGGL((k2_gram_syrk_bf16<NTC, k2_bf16_kc(NTC)>), g2, dim3(64 * K2_BF16_WAVES), 0, st, p16,    \
-                         rows, ld_panel, D.d_tiles, D.ngroups, ks, D.nslots, accumulate, slab);                   \
-    }                                                                                                             \
-    break;
-    SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
-    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
-    SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20)
-    SYSID_K2_CASE(15, 20) SYSID_K2_CASE(16, 12) SYSID_K2_CASE(17, 12) SYSID_K2_CASE(18, 12)
-    SYSID_K2_CASE(19, 12) SYSID_K2_CASE(20, 12) SYSID_K2_CASE(21, 8) SYSID_K2_CASE(22, 8)
-    SYSID_K2_CASE(23, 8) SYSID_K2_CASE(24, 8)
-#undef SYSID_K2_CASE
-#undef SYSID_K2_F64
-#undef SYSID_K2_F32
-#undef SYSID_K2_DMA_LAUNCH
-#undef SYSID_K2_BLK
-    default:
-      return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
-  }
+  const sysid_engine::Deal& D = sx.in ? e->k2s : e->k2d[prec];
+  const sysid_launch::K2Args a{e->ntc, D.d_tiles, D.ngroups, D.nslots, D.blk, d_panel, rows, ld_panel, ks,
+                               accumulate, slab, st, rowlist, d_rows, sx};
+  // the instantiation unit of (Gram arithmetic, width class)
+  static constexpr bool (*k2l[6])(const sysid_launch::K2Args&) = {
+      sysid_launch::k2_launch<0, 0>, sysid_launch::k2_launch<0, 1>, sysid_launch::k2_launch<1, 0>,
+      sysid_launch::k2_launch<1, 1>, sysid_launch::k2_launch<2, 0>, sysid_launch::k2_launch<2, 1>};
+  const bool ok = k2l[prec * 2 + (e->ntc >= 16 ? 1 : 0)](a);
+  if (!ok) return set_err(e, SYSID_E_MODEL, "Gram width %d columns is not supported (max 384)", e->ncol);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
 
-int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st, int prec = 0) {
-  const sysid_engine::Deal& D = e->k2d[prec];  // the slabs follow the K2 kernel's own deal
+int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st, int prec = 0,
+              bool structured = false) {
+  const sysid_engine::Deal& D = structured ? e->k2s : e->k2d[prec];  // the slabs follow the K2 kernel's own deal
   const int64_t nx = (int64_t)D.nslots * 256;
   const int2* tiles = D.d_tiles + D.nsuper;
   hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, tiles, nx, ks, e->ncol,
@@ -403,6 +272,13 @@ int check_stages(sysid_engine* e, int64_t N, int64_t ld_panel, uint32_t flags, c
   return SYSID_OK;
 }
 
+// The structured-Gram arguments of a projector-row panel of N samples (inputs d_in, leading dimension ld), or
+// K2Struct{} when the model has no structured deal.
+K2Struct k2_struct(const sysid_engine* e, const double* d_in, int64_t ld, int64_t N) {
+  if (e->k2s.ngroups == 0) return K2Struct{};
+  return K2Struct{d_in, ld, N, e->nq + e->kp.bd, e->nq + 2 * e->nv, e->wy + e->nj, e->k2s_ntm, e->k2s_slot0};
+}
+
 int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                   int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, hipStream_t st,
                   hipEvent_t* ev /* 4 events or null */) {
@@ -417,9 +293,12 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   if (flags & SYSID_EMIT_GRAM) {
     const int ks = ksplit_for(e, rows);
     double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, gram_prec(flags))) != SYSID_OK) return rc;
+    const int prec = gram_prec(flags);
+    const K2Struct sx = prec == 0 ? k2_struct(e, d_in, ld, N) : K2Struct{};
+    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, prec, nullptr, nullptr, sx)) != SYSID_OK)
+      return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
-    if ((rc = launch_k3(e, ks, slab, d_gram, st)) != SYSID_OK) return rc;
+    if ((rc = launch_k3(e, ks, slab, d_gram, st, prec, sx.in != nullptr)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
   } else if (ev) {
     HIP_TRY(e, hipEventRecord(ev[2], st));
@@ -737,8 +616,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   // K2W x K2S super slots per workgroup group; 4 tile slots per super slot.
   e->ntc = (e->ncol + 15) / 16;
   // K2W waves x K2S super slots per workgroup group -> d_tiles = [super slots | tile slots]
-  auto deal = [&](int K2W, int K2S, int& ngroups, int& nsuper, int& nslots) -> std::vector<int2> {
-    const int nsg = (e->ntc + 1) / 2;
+  auto deal = [&](int K2W, int K2S, int& ngroups, int& nsuper, int& nslots, int ntx) -> std::vector<int2> {
+    const int nsg = (ntx + 1) / 2;
     std::vector<int2> sl;
     for (int I0 = 0; I0 < nsg; ++I0)
       for (int J0 = I0; J0 < nsg; ++J0) sl.push_back(int2{I0, J0});
@@ -753,7 +632,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
         for (int a = 0; a < 2; ++a)
           for (int b = 0; b < 2; ++b) {
             const int I0 = 2 * t.x + a, J0 = 2 * t.y + b;
-            n += (I0 <= J0 && J0 < e->ntc) ? 1 : 0;
+            n += (I0 <= J0 && J0 < ntx) ? 1 : 0;
           }
         return n;
       };
@@ -839,7 +718,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) {
           const int I0 = 2 * sl[k].x + a, J0 = 2 * sy + b;
-          if (I0 <= J0 && I0 < e->ntc && J0 < e->ntc && !((skip >> (2 * a + b)) & 1)) tl[4 * k + 2 * a + b] = int2{I0, J0};
+          if (I0 <= J0 && I0 < ntx && J0 < ntx && !((skip >> (2 * a + b)) & 1)) tl[4 * k + 2 * a + b] = int2{I0, J0};
         }
     }
     nslots = (int)tl.size();
@@ -854,7 +733,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     sysid_engine::Deal& D = e->k2d[p];
     const int w = p == 2 ? K2_BF16_WAVES : k2_waves(e->ntc);
     const int sp = p == 0 ? k2_slots<double>(e->ntc) : p == 1 ? k2_slots<float>(e->ntc) : k2_bf16_spw(e->ntc);
-    dealt[p] = deal(w, sp, D.ngroups, D.nsuper, D.nslots);
+    dealt[p] = deal(w, sp, D.ngroups, D.nsuper, D.nslots, e->ntc);
     if (k2b_supported(e->ntc)) {
       // the register-blocked kernels: no super-tile slots, the roles' tiles in slab order (8 roles per group;
       // f64 two groups, f32 / bf16 one)
@@ -873,6 +752,26 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     }
   }
 
+  // The structured f64 Gram (k2_gram_syrk<double, 10, 32, 18, 2>): nv = 18 floating-base models with 13 bodies
+  // (Spot, solo12: B_v and B_c 0..1 end inside the MFMA tile columns [0, 9), B_c 2..11 and tau_proj fill tile
+  // column 9).
+  std::vector<int2> dealt_s;
+  {
+    const int ntm = (e->wy + e->nj + 15) / 16;
+    const char* env = std::getenv("SYSID_K2_STRUCT");  // A/B switch: 0 = the dense deal
+    const bool on = !(env && std::atoi(env) == 0);
+    if (on && e->nv == 18 && e->kp.bd == 6 && e->nj == 12 && e->ntc == 10 && ntm == 9 &&
+        16 * ntm - (e->wy + e->nj) == 2 && e->wy + 2 * e->nj + 1 == e->ncol) {
+      sysid_engine::Deal& D = e->k2s;
+      dealt_s = deal(k2_waves(e->ntc), k2_slots<double>(e->ntc), D.ngroups, D.nsuper, D.nslots, ntm);
+      e->k2s_ntm = ntm;
+      e->k2s_slot0 = D.nslots;
+      for (int J = ntm; J < e->ntc; ++J)
+        for (int I = 0; I <= J; ++I) dealt_s.push_back(int2{I, J});
+      D.nslots = (int)dealt_s.size() - D.nsuper;
+    }
+  }
+
   hipError_t st = hipSetDevice(device);
   hipDeviceProp_t prop;
   if (st == hipSuccess) st = hipGetDeviceProperties(&prop, device);
@@ -887,6 +786,11 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     int2*& t = e->k2d[p].d_tiles;
     if (st == hipSuccess) st = hipMalloc(&t, dealt[p].size() * sizeof(int2));
     if (st == hipSuccess) st = hipMemcpy(t, dealt[p].data(), dealt[p].size() * sizeof(int2), hipMemcpyHostToDevice);
+  }
+  if (st == hipSuccess && !dealt_s.empty()) {
+    st = hipMalloc(&e->k2s.d_tiles, dealt_s.size() * sizeof(int2));
+    if (st == hipSuccess)
+      st = hipMemcpy(e->k2s.d_tiles, dealt_s.data(), dealt_s.size() * sizeof(int2), hipMemcpyHostToDevice);
   }
   // K1 shapes: per instantiation, the waves per workgroup that maximise resident waves per CU under the LDS
   // budget.  Layout candidates of the projector rows: the Q-form when it applies (less arithmetic, no P slot),
@@ -952,7 +856,7 @@ void sysid_destroy(sysid_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_in, (void*)e->d_panel,
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->k2s.d_tiles, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1365,6 +1269,15 @@ int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4) {
   cfg4[1] = e->k1m[0].bpc;
   cfg4[2] = (int32_t)e->k1m[0].lds;
   cfg4[3] = e->k1_maxch_tpl;
+  return SYSID_OK;
+}
+
+int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4) {
+  if (!e || !cfg4) return SYSID_E_INVALID;
+  cfg4[0] = e->ntc;
+  cfg4[1] = e->k2s.ngroups > 0 ? e->k2s_ntm : 0;
+  cfg4[2] = e->k2d[0].nslots;
+  cfg4[3] = e->k2s.nslots;
   return SYSID_OK;
 }
 

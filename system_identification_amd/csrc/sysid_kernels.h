@@ -1,6 +1,7 @@
 // sysid_kernels.h — device code of the MI355X identification-regressor engine (gfx950, wave64).
 //
-// Included once, by sysid_engine.hip.  Kernels:
+// Included by sysid_engine.hip (every kernel) and by the instantiation units sysid_k1_inst.hip /
+// sysid_k2_inst.hip (SYSID_TEMPLATE_TU: the templates only, one panel type each).  Kernels:
 //   k1_regressor_panel  per sample: forward kinematics, contact Jacobian, projector P, projected
 //                       regressor / friction / torque columns -> panel [Y_proj | B_v | B_c | tau_proj].
 //                       One wave = one sample; a workgroup holds 4 independent waves; no workgroup
@@ -1636,6 +1637,7 @@ __device__ __forceinline__ int k1s_wave_incl(int v, int lane) {  // inclusive sc
   return v;
 }
 
+#ifndef SYSID_TEMPLATE_TU  // the non-template kernels live in sysid_engine.hip's translation unit only
 __global__ void __launch_bounds__(256)
 k1s_seg_sums(const int* __restrict__ rcount, int n, int* __restrict__ rseg) {
   __shared__ int wsum[4];
@@ -1683,6 +1685,8 @@ k1s_row_list(const int* __restrict__ rcount, const int* __restrict__ rseg, int n
   }
   if (b == (int)gridDim.x - 1 && t == 255) *total = o;
 }
+
+#endif  // SYSID_TEMPLATE_TU
 
 // ------------------------------------------------------------------------------------------------
 // K2: G_partial[ks] = panel[rows of ks]^T panel[rows of ks]   (fp64 MFMA 16x16x4, upper tiles)
@@ -1764,12 +1768,36 @@ __host__ __device__ constexpr int k2_bf16_kc(int ntc) {
                                                           : ((150 * 1024 / (64 * ntc)) - 8) / 32 * 32;
 }
 
-template <typename T, int NTC, int KC>
+// Structured Gram columns (NVS > 0: the nv = NVS floating-base models' projector-row panels).  Every panel
+// column is in P's range (P A = A), and B_v, B_c and the torque column are P Sᵀ times per-joint scalars, so
+// the Gram's columns of B_c_j and tau_proj need no dot product over all rows:
+//   Aᵀ B_c[:, j] = Aᵀ P S e_j sign(dq_j) = (P A)ᵀ e_{6+j} sign(dq_j) = Σ_samples sign(dq_j) · A[6+j, :]ᵀ,
+//   Aᵀ tau_proj  = Σ_samples Σ_j tau_j · A[6+j, :]ᵀ                         (src/sys_identification.py:401-418)
+// The MFMA deal then covers only the tile columns [0, ntm) (Y_proj and B_v), and the tile columns [ntm, NTC)
+// are accumulated by the first three waves on the VALU from the same staged rows: lane r (Gram row r) adds
+// A[R, r] · sign(dq_j) to its B_c_j accumulator and A[R, r] · tau_j to its torque one for every joint row R
+// (joint j) of the chunk.  Spot: 45 of 55 tiles on MFMA (busiest SIMD 14 -> 12).  dq / tau come from the
+// channel-major input block, one chunk ahead (lane q·NJ + j holds sample q's joint j).
+struct K2Struct {
+  const double* in;  // channel-major inputs [q; dq; ddq; tau; contact] (nullptr: structured mode off)
+  int64_t ldin;      // input leading dimension (samples)
+  int64_t nsamp;     // samples of the panel
+  int ch_dq, ch_tau; // channel of dq[6] (joint 0) and of tau[0]
+  int bc0;           // panel column of B_c_0 (= wy + nj); tau_proj is bc0 + nj
+  int ntm;           // MFMA tile columns (B_c / tau columns at or past 16 ntm are structured)
+  int slot0;         // slab slot of the first structured tile: tiles (I, J), J in [ntm, NTC), I <= J, by J then I
+};
+
+template <typename T, int NTC, int KC, int NVS = 0, int JS0 = 0>
 __global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
-             int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+             int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab, K2Struct sx) {
   typedef typename K2Acc<T>::type accT;
   constexpr int K2W = k2_waves(NTC), K2S = k2_slots<T>(NTC);
+  static_assert(NVS == 0 || (sizeof(T) == 8 && 3 * 64 >= 16 * NTC && 3 * (NVS - 6) <= 64 && JS0 < NVS - 6),
+                "structured shape");
+  constexpr int NJS = NVS > 0 ? NVS - 6 : 1;                // joints of the structured mode
+  const int ntm = NVS > 0 ? sx.ntm : NTC;
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;                       // elements per LDS buffer
   constexpr int NT = 64 * K2W;
@@ -1828,7 +1856,7 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int I = 2 * sp.x + (t >> 1), J = 2 * (sp.y & 0xFF) + (t & 1);
-      need[s][t] = live[s] && I <= J && J < NTC && !k2_tile_skip(sp, t);
+      need[s][t] = live[s] && I <= J && J < ntm && !k2_tile_skip(sp, t);
     }
     const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * (sp.y & 0xFF), 2 * (sp.y & 0xFF) + 1};
 #pragma unroll
@@ -1842,6 +1870,48 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   for (int s = 0; s < K2S; ++s)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
+
+  // structured columns (NVS > 0): waves 0..2, lane r = Gram row r
+  constexpr int NVD = NVS > 0 ? NVS : 1;
+  const bool sw = NVS > 0 && wave < 3;  // wave-uniform
+  const int sr = wave * 64 + lane;
+  double sbc[NJS - JS0], stau = 0.0;  // B_c_j for j >= JS0 (the B_c columns past the MFMA tiles), tau_proj
+#pragma unroll
+  for (int j = 0; j < NJS - JS0; ++j) sbc[j] = 0.0;
+  // dq_j and tau_j of sample c0 / NVS + q in lane q·NJS + j (0 past the samples)
+  auto struct_coef = [&](int64_t c0, double& dv, double& tv) {
+    const int q = lane / NJS, j = lane - q * NJS;
+    const int64_t smp = c0 / NVD + q;
+    dv = 0.0;
+    tv = 0.0;
+    if (lane < 3 * NJS && smp < sx.nsamp) {
+      dv = sx.in[(int64_t)(sx.ch_dq + j) * sx.ldin + smp];
+      tv = sx.in[(int64_t)(sx.ch_tau + j) * sx.ldin + smp];
+    }
+  };
+  // the joint rows of the chunk starting at panel row c0 (rows past the range are zero in LDS)
+  auto struct_chunk = [&](const T* cur, int64_t c0, double dv, double tv) {
+    const float sg = dv > 0.0 ? 1.0f : (dv < 0.0 ? -1.0f : 0.0f);  // sign(dq), sign(0) = 0
+    const int p = (int)(c0 % NVD);
+    const T* col = cur + sr;
+#pragma unroll
+    for (int j = 0; j < NJS; ++j) {
+      int kk = 6 + j - p;
+      if (kk < 0) kk += NVD;
+#pragma unroll
+      for (int o = 0; o < (KC + NVD - 1) / NVD; ++o) {
+        const int row = kk + NVD * o;
+        if (row < KC) {
+          const int q = (p + row) / NVD;
+          const double a = col[row * STRIDE];
+          stau += a * readlane_f64(tv, q * NJS + j);
+          if (j >= JS0)
+            sbc[j - JS0] += a * (double)__builtin_bit_cast(
+                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sg), q * NJS + j));
+        }
+      }
+    }
+  };
 
   // Loads run two chunks ahead through two register sets: chunk c + 2 is requested while chunk c is
   // multiplied and chunk c + 1 (requested one chunk earlier) is written to the other LDS buffer, so each
@@ -1888,6 +1958,16 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
     for (int u = 0; u < PER; ++u)
       if (used[u]) *reinterpret_cast<uint4*>(b + loff[u]) = S == 0 ? sa[u] : sb[u];
   };
+  // one chunk: its MFMAs are issued first, then (structured waves) the VALU columns while they run; the next
+  // chunk's coefficients are requested before this chunk's are used
+  auto chunk = [&](const T* cur, int64_t c0) {
+    double dv = 0.0, tv = 0.0;
+    if constexpr (NVS > 0)
+      if (sw) struct_coef(c0, dv, tv);  // lands while this chunk's MFMAs issue
+    mfma_chunk(cur);
+    if constexpr (NVS > 0)
+      if (sw) struct_chunk(cur, c0, dv, tv);
+  };
   constexpr std::integral_constant<int, 0> A{};
   constexpr std::integral_constant<int, 1> B{};
   __syncthreads();  // LDS zeroed
@@ -1900,23 +1980,23 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   int64_t c = 0;
   for (; c + 1 < nfull; c += 2) {  // chunks c (buffer 0, set A) and c + 1 (buffer 1, set B)
     load_full(c + 2, A);
-    mfma_chunk(lds);
+    chunk(lds, r0 + c * KC);
     store_set(B, lds + BUF);
     __syncthreads();
     load_full(c + 3, B);
-    mfma_chunk(lds + BUF);
+    chunk(lds + BUF, r0 + (c + 1) * KC);
     if (c + 2 < nfull) store_set(A, lds);
     __syncthreads();
   }
   if (c < nfull) {  // an odd last full chunk, already in buffer 0
-    mfma_chunk(lds);
+    chunk(lds, r0 + c * KC);
     __syncthreads();
   }
   if (r0 + nfull * KC < r1) {  // the panel's partial last chunk
     load_chunk(r0 + nfull * KC);
     store_chunk(lds);
     __syncthreads();
-    mfma_chunk(lds);
+    chunk(lds, r0 + nfull * KC);
   }
   // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
 #pragma unroll
@@ -1931,6 +2011,28 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
         double* x = o + row * 16 + (lane & 15);
         const double v = (double)acc[s][t][j];
         *x = accumulate ? *x + v : v;  // chunked Gram: slabs carry over chunks
+      }
+    }
+  }
+  if constexpr (NVS > 0) {
+    // structured tiles (I, J), J in [ntm, NTC), I <= J: lane r writes row r % 16 of tile (r / 16, J), its
+    // B_c / tau entries and zeros (wave-uniform column positions)
+    if (sw && sr < 16 * NTC) {
+      const int I = sr >> 4, rr = sr & 15;
+      int slot = sx.slot0;
+      for (int J = ntm; J < NTC; ++J) {
+        if (I <= J) {
+          double* o = slab + ((size_t)ks * nslots + (size_t)(slot + I)) * 256 + rr * 16;
+#pragma unroll
+          for (int x = 0; x < 16; ++x) {
+            const int jb = 16 * J + x - sx.bc0;  // B_c joint of column 16 J + x (tau: jb == NJS)
+            double w = jb == NJS ? stau : 0.0;
+#pragma unroll
+            for (int j = JS0; j < NJS; ++j) w = jb == j ? sbc[j - JS0] : w;
+            o[x] = accumulate ? o[x] + w : w;
+          }
+        }
+        slot += J + 1;
       }
     }
   }
@@ -2947,6 +3049,7 @@ k2_gram_syrk_blk(const T* __restrict__ panel, int64_t rows, int64_t ldp, int ksp
 #undef SYSID_K2X_WAVE
 }
 
+#ifndef SYSID_TEMPLATE_TU
 // K3, one pass: G = the sum of the ksplit slabs, in a fixed order, mirrored.  A workgroup of 16 waves owns 64
 // consecutive entries of one tile slot (so a dead slot drops the whole workgroup); wave w sums slabs w, w + 16,
 // ... with eight loads in flight per lane, and the 16 wave sums are added in LDS as a fixed pairwise tree.
@@ -2977,7 +3080,9 @@ k3_gram_reduce(const double* __restrict__ slab, const int2* __restrict__ tiles, 
   if (wave == 0) {
     const int x = (int)(e & 255);
     const int gi = ij.x * 16 + (x >> 4), gj = ij.y * 16 + (x & 15);
-    if (gi < ncol && gj < ncol) {
+    // a diagonal tile's upper half only: its two halves may differ by rounding (the structured tiles of
+    // k2_gram_syrk NVS > 0), and both entries write both mirrored positions
+    if (gi < ncol && gj < ncol && (ij.x != ij.y || (x >> 4) <= (x & 15))) {
       const double acc = red[0][lane];
       G[(int64_t)gi * ncol + gj] = acc;
       G[(int64_t)gj * ncol + gi] = acc;
@@ -3082,5 +3187,6 @@ __global__ void debug_body_column_kernel(const double* __restrict__ body24, doub
   block_column(F, threadIdx.x % 10, fw);
   for (int k = 0; k < 6; ++k) out[threadIdx.x * 6 + k] = fw[k];
 }
+#endif  // SYSID_TEMPLATE_TU
 
 }  // namespace sysid_dev

@@ -56,6 +56,7 @@ SIGNATURES = [
     ("sysid_debug_layout", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_debug_k1_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_gram_rows", _c.c_int32, [_vp, _c.c_uint32]),
+    ("sysid_debug_k2_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
@@ -379,6 +380,13 @@ class Engine:
         """K1 launch shape of the f64 panel [waves per workgroup, workgroups per CU, LDS bytes, chain slots]."""
         cfg = (ctypes.c_int32 * 4)()
         self._check(self.lib.sysid_debug_k1_config(self._h, cfg))
+        return list(cfg)
+
+    def k2_config(self) -> list:
+        """K2 Gram deal [tile columns, MFMA tile columns of the structured f64 Gram (0: none), dense f64 tile slots,
+        structured tile slots]; SYSID_K2_STRUCT=0 at model creation selects the dense deal."""
+        cfg = (ctypes.c_int32 * 4)()
+        self._check(self.lib.sysid_debug_k2_config(self._h, cfg))
         return list(cfg)
 
     def time_stages(self, d_in, N: int, flags: int, bufs: dict, iters: int = 10) -> list:
