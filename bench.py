@@ -312,14 +312,6 @@ def main():
         # nv-row count stays in K2_TFps / gram_gflops
         rows_per_sample = float(np.mean(nv - 3 * (data["contact"] != 0).sum(axis=0)))
     k2_exec_tfs = k2_tfs * rows_per_sample / nv
-    k2cfg = eng.k2_config()
-    structured = not args.gram_only and k2cfg[1] > 0
-    if structured:
-        # the structured f64 Gram (sysid_kernels.h K2Struct): the MFMA tiles cover the first 16·ntm columns, the
-        # B_c / tau_proj columns past them are VALU sums over the joint rows; roofline.achieved counts the MFMA
-        # SYRK it executes, K2_TFps / gram_gflops stay on §8(d)'s dense count
-        cm = 16 * k2cfg[1]
-        k2_exec_tfs = n_time * nv * cm * (cm + 1) / (ms[1] * 1e-3) / 1e12
     if ms[0] >= ms[1]:
         traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N) if not args.gram_only else (None, None)
         roof = {"kernel": "k1_regressor_panel", "bound": "hbm", "achieved": round(k1_gbs, 1),
@@ -332,10 +324,7 @@ def main():
         roof = {"kernel": "k2_gram_syrk", "bound": "mfma", "achieved": round(k2_exec_tfs, 3),
                 "peak": peak, "unit": "TFLOP/s", "frac": round(k2_exec_tfs / peak, 4),
                 "traffic": traffic, "traffic_source": src,
-                "algorithmic_flops_per_launch": round(n_time * nv * (16 * k2cfg[1]) * (16 * k2cfg[1] + 1)) if structured
-                else round(n_time * flops_k2 * rows_per_sample / nv),
-                "structured_gram": ({"mfma_columns": 16 * k2cfg[1], "valu_columns": f"{16 * k2cfg[1]}..{W}"}
-                                    if structured else None),
+                "algorithmic_flops_per_launch": round(n_time * flops_k2 * rows_per_sample / nv),
                 "rows_per_sample": round(rows_per_sample, 3), "avg_launch_ms": round(ms[1], 5)}
 
     ms_step = elapsed / args.steps * 1e3

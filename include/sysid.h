@@ -212,8 +212,7 @@ int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, cons
 int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12);
 /* K1 launch shape chosen at model creation: {waves per workgroup, workgroups per CU, LDS bytes, chain tpl}. */
 int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4);
-/* K2 Gram deal chosen at model creation: {tile columns, MFMA tile columns of the structured f64 deal (0: the
- * model has none; sysid_kernels.h K2Struct), f64 tile slots of the dense deal, of the structured deal}. */
+/* K2 Gram deal chosen at model creation: {tile columns, tile slots of the f64, f32 and bf16 deals}. */
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */
 int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6);

@@ -66,10 +66,6 @@ struct sysid_engine {
     int blk = 0;  // the register-blocked kernel (k2_gram_syrk_blk / _bf16_blk): one workgroup per CU
     int2* d_tiles = nullptr;  // [super slots | tile slots]
   } k2d[3];
-  // structured f64 Gram (k2_gram_syrk NVS = 18: B_c / tau tile columns on the VALU, sysid_kernels.h K2Struct):
-  // its own deal of the MFMA tile columns [0, k2s_ntm) plus the structured tiles (k2s.ngroups == 0: not used)
-  Deal k2s;
-  int k2s_ntm = 0, k2s_slot0 = 0;
   // host-API buffers (grow-only)
   double* d_in = nullptr;
   size_t in_cap = 0;
@@ -116,8 +112,7 @@ int ksplit_for(const sysid_engine* e, int64_t rows, int prec = 0) {
 }
 
 size_t slab_bytes(const sysid_engine* e, int64_t rows, int prec = 0) {
-  const int nslots = std::max(e->k2d[prec].nslots, prec == 0 ? e->k2s.nslots : 0);  // either f64 deal
-  return align256((size_t)ksplit_for(e, rows, prec) * nslots * 256 * sizeof(double));
+  return align256((size_t)ksplit_for(e, rows, prec) * e->k2d[prec].nslots * 256 * sizeof(double));
 }
 
 int grow(sysid_engine* e, void** p, size_t* cap, size_t need) {
@@ -219,15 +214,13 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
 
 // rowlist / d_rows: the nullspace mode's gathered rows (k1s_row_list; `rows` is then only the bound the split
 // was sized for): the LDS-DMA / blocked kernels for every width and arithmetic (sysid_k2_inst.hip).
-// sx: the structured f64 Gram (sx.in != nullptr; the engine's k2s deal), else the arithmetic's own deal.
 int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_panel, int ks, int accumulate,
-              double* slab, hipStream_t st, int prec, const int* rowlist = nullptr, const int* d_rows = nullptr,
-              const K2Struct& sx = K2Struct{}) {
+              double* slab, hipStream_t st, int prec, const int* rowlist = nullptr, const int* d_rows = nullptr) {
   if (ld_panel > 16 * e->ntc)
     return set_err(e, SYSID_E_INVALID, "Gram path needs ld_panel <= %d (16-column tiles)", 16 * e->ntc);
-  const sysid_engine::Deal& D = sx.in ? e->k2s : e->k2d[prec];
+  const sysid_engine::Deal& D = e->k2d[prec];
   const sysid_launch::K2Args a{e->ntc, D.d_tiles, D.ngroups, D.nslots, D.blk, d_panel, rows, ld_panel, ks,
-                               accumulate, slab, st, rowlist, d_rows, sx};
+                               accumulate, slab, st, rowlist, d_rows};
   // the instantiation unit of (Gram arithmetic, width class)
   static constexpr bool (*k2l[6])(const sysid_launch::K2Args&) = {
       sysid_launch::k2_launch<0, 0>, sysid_launch::k2_launch<0, 1>, sysid_launch::k2_launch<1, 0>,
@@ -238,9 +231,8 @@ int launch_k2(sysid_engine* e, const void* d_panel, int64_t rows, int64_t ld_pan
   return SYSID_OK;
 }
 
-int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st, int prec = 0,
-              bool structured = false) {
-  const sysid_engine::Deal& D = structured ? e->k2s : e->k2d[prec];  // the slabs follow the K2 kernel's own deal
+int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipStream_t st, int prec = 0) {
+  const sysid_engine::Deal& D = e->k2d[prec];  // the slabs follow the K2 kernel's own deal
   const int64_t nx = (int64_t)D.nslots * 256;
   const int2* tiles = D.d_tiles + D.nsuper;
   hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, tiles, nx, ks, e->ncol,
@@ -272,13 +264,6 @@ int check_stages(sysid_engine* e, int64_t N, int64_t ld_panel, uint32_t flags, c
   return SYSID_OK;
 }
 
-// The structured-Gram arguments of a projector-row panel of N samples (inputs d_in, leading dimension ld), or
-// K2Struct{} when the model has no structured deal.
-K2Struct k2_struct(const sysid_engine* e, const double* d_in, int64_t ld, int64_t N) {
-  if (e->k2s.ngroups == 0) return K2Struct{};
-  return K2Struct{d_in, ld, N, e->nq + e->kp.bd, e->nq + 2 * e->nv, e->wy + e->nj, e->k2s_ntm, e->k2s_slot0};
-}
-
 int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                   int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, hipStream_t st,
                   hipEvent_t* ev /* 4 events or null */) {
@@ -294,11 +279,9 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
     const int ks = ksplit_for(e, rows);
     double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
     const int prec = gram_prec(flags);
-    const K2Struct sx = prec == 0 ? k2_struct(e, d_in, ld, N) : K2Struct{};
-    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, prec, nullptr, nullptr, sx)) != SYSID_OK)
-      return rc;
+    if ((rc = launch_k2(e, d_panel, rows, ld_panel, ks, 0, slab, st, prec)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[2], st));
-    if ((rc = launch_k3(e, ks, slab, d_gram, st, prec, sx.in != nullptr)) != SYSID_OK) return rc;
+    if ((rc = launch_k3(e, ks, slab, d_gram, st, prec)) != SYSID_OK) return rc;
     if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
   } else if (ev) {
     HIP_TRY(e, hipEventRecord(ev[2], st));
@@ -752,26 +735,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     }
   }
 
-  // The structured f64 Gram (k2_gram_syrk<double, 10, 32, 18, 2>): nv = 18 floating-base models with 13 bodies
-  // (Spot, solo12: B_v and B_c 0..1 end inside the MFMA tile columns [0, 9), B_c 2..11 and tau_proj fill tile
-  // column 9).
-  std::vector<int2> dealt_s;
-  {
-    const int ntm = (e->wy + e->nj + 15) / 16;
-    const char* env = std::getenv("SYSID_K2_STRUCT");  // A/B switch: 0 = the dense deal
-    const bool on = !(env && std::atoi(env) == 0);
-    if (on && e->nv == 18 && e->kp.bd == 6 && e->nj == 12 && e->ntc == 10 && ntm == 9 &&
-        16 * ntm - (e->wy + e->nj) == 2 && e->wy + 2 * e->nj + 1 == e->ncol) {
-      sysid_engine::Deal& D = e->k2s;
-      dealt_s = deal(k2_waves(e->ntc), k2_slots<double>(e->ntc), D.ngroups, D.nsuper, D.nslots, ntm);
-      e->k2s_ntm = ntm;
-      e->k2s_slot0 = D.nslots;
-      for (int J = ntm; J < e->ntc; ++J)
-        for (int I = 0; I <= J; ++I) dealt_s.push_back(int2{I, J});
-      D.nslots = (int)dealt_s.size() - D.nsuper;
-    }
-  }
-
   hipError_t st = hipSetDevice(device);
   hipDeviceProp_t prop;
   if (st == hipSuccess) st = hipGetDeviceProperties(&prop, device);
@@ -786,11 +749,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     int2*& t = e->k2d[p].d_tiles;
     if (st == hipSuccess) st = hipMalloc(&t, dealt[p].size() * sizeof(int2));
     if (st == hipSuccess) st = hipMemcpy(t, dealt[p].data(), dealt[p].size() * sizeof(int2), hipMemcpyHostToDevice);
-  }
-  if (st == hipSuccess && !dealt_s.empty()) {
-    st = hipMalloc(&e->k2s.d_tiles, dealt_s.size() * sizeof(int2));
-    if (st == hipSuccess)
-      st = hipMemcpy(e->k2s.d_tiles, dealt_s.data(), dealt_s.size() * sizeof(int2), hipMemcpyHostToDevice);
   }
   // K1 shapes: per instantiation, the waves per workgroup that maximise resident waves per CU under the LDS
   // budget.  Layout candidates of the projector rows: the Q-form when it applies (less arithmetic, no P slot),
@@ -856,7 +814,7 @@ void sysid_destroy(sysid_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->k2s.d_tiles, (void*)e->d_in, (void*)e->d_panel,
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1275,9 +1233,9 @@ int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4) {
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4) {
   if (!e || !cfg4) return SYSID_E_INVALID;
   cfg4[0] = e->ntc;
-  cfg4[1] = e->k2s.ngroups > 0 ? e->k2s_ntm : 0;
-  cfg4[2] = e->k2d[0].nslots;
-  cfg4[3] = e->k2s.nslots;
+  cfg4[1] = e->k2d[0].nslots;
+  cfg4[2] = e->k2d[1].nslots;
+  cfg4[3] = e->k2d[2].nslots;
   return SYSID_OK;
 }
 

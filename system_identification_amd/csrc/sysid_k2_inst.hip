@@ -46,15 +46,8 @@ void k2_case(const K2Args& a) {
                          a.ngroups, a.ks, a.nslots, a.accumulate, a.slab, a.rowlist, a.d_rows);
     } else {
       constexpr int RKC = (PREC == 0 ? 1 : 2) * KC;
-      if constexpr (PREC == 0 && NTC == 10) {
-        if (a.sx.in != nullptr) {  // structured B_c / tau columns (nv = 18, 13 bodies: Spot, solo12; B_c 0..1 on MFMA)
-          hipLaunchKernelGGL((k2_gram_syrk<E, NTC, RKC, 18, 2>), g2, b2, 0, a.st, P, a.rows, a.ld_panel, T,
-                             a.ngroups, a.ks, a.nslots, a.accumulate, a.slab, a.sx);
-          return;
-        }
-      }
       hipLaunchKernelGGL((k2_gram_syrk<E, NTC, RKC>), g2, b2, 0, a.st, P, a.rows, a.ld_panel, T, a.ngroups, a.ks,
-                         a.nslots, a.accumulate, a.slab, K2Struct{});
+                         a.nslots, a.accumulate, a.slab);
     }
   } else {
     const __bf16* P = static_cast<const __bf16*>(a.panel);

@@ -1768,36 +1768,12 @@ __host__ __device__ constexpr int k2_bf16_kc(int ntc) {
                                                           : ((150 * 1024 / (64 * ntc)) - 8) / 32 * 32;
 }
 
-// Structured Gram columns (NVS > 0: the nv = NVS floating-base models' projector-row panels).  Every panel
-// column is in P's range (P A = A), and B_v, B_c and the torque column are P Sᵀ times per-joint scalars, so
-// the Gram's columns of B_c_j and tau_proj need no dot product over all rows:
-//   Aᵀ B_c[:, j] = Aᵀ P S e_j sign(dq_j) = (P A)ᵀ e_{6+j} sign(dq_j) = Σ_samples sign(dq_j) · A[6+j, :]ᵀ,
-//   Aᵀ tau_proj  = Σ_samples Σ_j tau_j · A[6+j, :]ᵀ                         (src/sys_identification.py:401-418)
-// The MFMA deal then covers only the tile columns [0, ntm) (Y_proj and B_v), and the tile columns [ntm, NTC)
-// are accumulated by the first three waves on the VALU from the same staged rows: lane r (Gram row r) adds
-// A[R, r] · sign(dq_j) to its B_c_j accumulator and A[R, r] · tau_j to its torque one for every joint row R
-// (joint j) of the chunk.  Spot: 45 of 55 tiles on MFMA (busiest SIMD 14 -> 12).  dq / tau come from the
-// channel-major input block, one chunk ahead (lane q·NJ + j holds sample q's joint j).
-struct K2Struct {
-  const double* in;  // channel-major inputs [q; dq; ddq; tau; contact] (nullptr: structured mode off)
-  int64_t ldin;      // input leading dimension (samples)
-  int64_t nsamp;     // samples of the panel
-  int ch_dq, ch_tau; // channel of dq[6] (joint 0) and of tau[0]
-  int bc0;           // panel column of B_c_0 (= wy + nj); tau_proj is bc0 + nj
-  int ntm;           // MFMA tile columns (B_c / tau columns at or past 16 ntm are structured)
-  int slot0;         // slab slot of the first structured tile: tiles (I, J), J in [ntm, NTC), I <= J, by J then I
-};
-
-template <typename T, int NTC, int KC, int NVS = 0, int JS0 = 0>
+template <typename T, int NTC, int KC>
 __global__ void __launch_bounds__(64 * k2_waves(NTC))
 k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
-             int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab, K2Struct sx) {
+             int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
   typedef typename K2Acc<T>::type accT;
   constexpr int K2W = k2_waves(NTC), K2S = k2_slots<T>(NTC);
-  static_assert(NVS == 0 || (sizeof(T) == 8 && 3 * 64 >= 16 * NTC && 3 * (NVS - 6) <= 64 && JS0 < NVS - 6),
-                "structured shape");
-  constexpr int NJS = NVS > 0 ? NVS - 6 : 1;                // joints of the structured mode
-  const int ntm = NVS > 0 ? sx.ntm : NTC;
   constexpr int STRIDE = k2_stride(NTC);
   constexpr int BUF = KC * STRIDE;                       // elements per LDS buffer
   constexpr int NT = 64 * K2W;
@@ -1845,100 +1821,34 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
       if (used[u]) *reinterpret_cast<uint4*>(b + loff[u]) = st[u];
   };
 
-  // fragment columns of this wave: f = 4*s + {I0, I0+1, J0, J0+1} (16-column blocks)
-  int foff[4 * K2S];
-  bool live[K2S];
-  bool need[K2S][4];  // wave-uniform: skip the lower tile of a diagonal super-tile, tiles past NTC
-#pragma unroll
-  for (int s = 0; s < K2S; ++s) {
-    int2 sp = supers[sbase + s];
-    live[s] = sp.x >= 0;
+  // One super-tile slot per wave (K2S = 1: this kernel serves the narrow Grams, < 16 tile columns).  Its
+  // fragment columns are {I0, I0+1, J0, J0+1} (16-column blocks) and its tile mask (tile t = 2a + b is (I0 + a,
+  // J0 + b); a diagonal super-tile skips its lower tile, tiles past NTC and a split super-tile's other half are
+  // skipped) is wave-uniform.  The chunk loop below is instantiated once per mask and selected by one scalar
+  // switch, so the k-loop is straight-line MFMAs: a per-tile `if (need)` on a value the compiler could not prove
+  // uniform had wrapped every MFMA in an exec-mask save / branch / restore (3.4 SALU + 1.4 branches per MFMA,
+  // profiles/r03_pmc) with an lgkmcnt(0) in front of it, and serialised the fragment reads of consecutive k-steps.
+  static_assert(K2S == 1, "one super-tile slot per wave");
+  const int2 sp = supers[sbase];
+  int foff[4];
+  int mask = 0;
+  {
+    const bool live = sp.x >= 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int I = 2 * sp.x + (t >> 1), J = 2 * (sp.y & 0xFF) + (t & 1);
-      need[s][t] = live[s] && I <= J && J < ntm && !k2_tile_skip(sp, t);
+      mask |= (live && I <= J && J < NTC && !k2_tile_skip(sp, t)) ? 1 << t : 0;
     }
     const int blk[4] = {2 * sp.x, 2 * sp.x + 1, 2 * (sp.y & 0xFF), 2 * (sp.y & 0xFF) + 1};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int b = live[s] && blk[u] < NTC ? blk[u] : 0;
-      foff[4 * s + u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
+      const int b = live && blk[u] < NTC ? blk[u] : 0;
+      foff[u] = (lane >> 4) * STRIDE + 16 * b + (lane & 15);
     }
   }
-  accT acc[K2S][4];
-#pragma unroll
-  for (int s = 0; s < K2S; ++s)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[s][t] = accT{0, 0, 0, 0};
+  mask = __builtin_amdgcn_readfirstlane(mask);
+  const bool live = sp.x >= 0;
 
-  // structured columns (NVS > 0): waves 0..2, lane r = Gram row r
-  constexpr int NVD = NVS > 0 ? NVS : 1;
-  const bool sw = NVS > 0 && wave < 3;  // wave-uniform
-  const int sr = wave * 64 + lane;
-  double sbc[NJS - JS0], stau = 0.0;  // B_c_j for j >= JS0 (the B_c columns past the MFMA tiles), tau_proj
-#pragma unroll
-  for (int j = 0; j < NJS - JS0; ++j) sbc[j] = 0.0;
-  // dq_j and tau_j of sample c0 / NVS + q in lane q·NJS + j (0 past the samples)
-  auto struct_coef = [&](int64_t c0, double& dv, double& tv) {
-    const int q = lane / NJS, j = lane - q * NJS;
-    const int64_t smp = c0 / NVD + q;
-    dv = 0.0;
-    tv = 0.0;
-    if (lane < 3 * NJS && smp < sx.nsamp) {
-      dv = sx.in[(int64_t)(sx.ch_dq + j) * sx.ldin + smp];
-      tv = sx.in[(int64_t)(sx.ch_tau + j) * sx.ldin + smp];
-    }
-  };
-  // the joint rows of the chunk starting at panel row c0 (rows past the range are zero in LDS)
-  auto struct_chunk = [&](const T* cur, int64_t c0, double dv, double tv) {
-    const float sg = dv > 0.0 ? 1.0f : (dv < 0.0 ? -1.0f : 0.0f);  // sign(dq), sign(0) = 0
-    const int p = (int)(c0 % NVD);
-    const T* col = cur + sr;
-#pragma unroll
-    for (int j = 0; j < NJS; ++j) {
-      int kk = 6 + j - p;
-      if (kk < 0) kk += NVD;
-#pragma unroll
-      for (int o = 0; o < (KC + NVD - 1) / NVD; ++o) {
-        const int row = kk + NVD * o;
-        if (row < KC) {
-          const int q = (p + row) / NVD;
-          const double a = col[row * STRIDE];
-          stau += a * readlane_f64(tv, q * NJS + j);
-          if (j >= JS0)
-            sbc[j - JS0] += a * (double)__builtin_bit_cast(
-                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sg), q * NJS + j));
-        }
-      }
-    }
-  };
-
-  // Loads run two chunks ahead through two register sets: chunk c + 2 is requested while chunk c is
-  // multiplied and chunk c + 1 (requested one chunk earlier) is written to the other LDS buffer, so each
-  // load has about two chunks of MFMA time to land.  Every load is unconditional (past the last full chunk
-  // the index is clamped: a reload of a chunk just read, from L2), so the compiler's vmcnt bookkeeping
-  // waits only for the set being stored.  The partial tail chunk of the panel's last workgroup runs last,
-  // zero-filled.
-  auto mfma_chunk = [&](const T* cur) {
-#pragma unroll
-    for (int kk = 0; kk < KC; kk += 4) {
-      T x[4 * K2S];
-#pragma unroll
-      for (int u = 0; u < 4 * K2S; ++u) x[u] = cur[foff[u] + kk * STRIDE];
-#pragma unroll
-      for (int s = 0; s < K2S; ++s) {
-        constexpr int AB[4][2] = {{0, 2}, {0, 3}, {1, 2}, {1, 3}};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (!need[s][t]) continue;
-          if constexpr (sizeof(T) == 8)
-            acc[s][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
-          else
-            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[4 * s + AB[t][0]], x[4 * s + AB[t][1]], acc[s][t], 0, 0, 0);
-        }
-      }
-    }
-  };
   const int64_t nfull = (r1 - r0) / KC;
   uint4 sa[PER], sb[PER];  // the two staging register sets (selected at compile time)
   auto load_full = [&](int64_t c, auto set) {
@@ -1958,83 +1868,96 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
     for (int u = 0; u < PER; ++u)
       if (used[u]) *reinterpret_cast<uint4*>(b + loff[u]) = S == 0 ? sa[u] : sb[u];
   };
-  // one chunk: its MFMAs are issued first, then (structured waves) the VALU columns while they run; the next
-  // chunk's coefficients are requested before this chunk's are used
-  auto chunk = [&](const T* cur, int64_t c0) {
-    double dv = 0.0, tv = 0.0;
-    if constexpr (NVS > 0)
-      if (sw) struct_coef(c0, dv, tv);  // lands while this chunk's MFMAs issue
-    mfma_chunk(cur);
-    if constexpr (NVS > 0)
-      if (sw) struct_chunk(cur, c0, dv, tv);
-  };
-  constexpr std::integral_constant<int, 0> A{};
-  constexpr std::integral_constant<int, 1> B{};
-  __syncthreads();  // LDS zeroed
-  if (nfull > 0) {
-    load_full(0, A);
-    load_full(1, B);
-    store_set(A, lds);
-  }
-  __syncthreads();
-  int64_t c = 0;
-  for (; c + 1 < nfull; c += 2) {  // chunks c (buffer 0, set A) and c + 1 (buffer 1, set B)
-    load_full(c + 2, A);
-    chunk(lds, r0 + c * KC);
-    store_set(B, lds + BUF);
-    __syncthreads();
-    load_full(c + 3, B);
-    chunk(lds + BUF, r0 + (c + 1) * KC);
-    if (c + 2 < nfull) store_set(A, lds);
-    __syncthreads();
-  }
-  if (c < nfull) {  // an odd last full chunk, already in buffer 0
-    chunk(lds, r0 + c * KC);
-    __syncthreads();
-  }
-  if (r0 + nfull * KC < r1) {  // the panel's partial last chunk
-    load_chunk(r0 + nfull * KC);
-    store_chunk(lds);
-    __syncthreads();
-    chunk(lds, r0 + nfull * KC);
-  }
-  // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
+
+  // Loads run two chunks ahead through two register sets: chunk c + 2 is requested while chunk c is
+  // multiplied and chunk c + 1 (requested one chunk earlier) is written to the other LDS buffer, so each
+  // load has about two chunks of MFMA time to land.  Every load is unconditional (past the last full chunk
+  // the index is clamped: a reload of a chunk just read, from L2), so the compiler's vmcnt bookkeeping
+  // waits only for the set being stored.  The partial tail chunk of the panel's last workgroup runs last,
+  // zero-filled.
+  auto run = [&](auto mc) {
+    constexpr int M = decltype(mc)::value;
+    // fragments the mask reads: A0 = I0 (tiles 0, 1), A1 = I0 + 1 (2, 3), B0 = J0 (0, 2), B1 = J0 + 1 (1, 3)
+    constexpr bool uA0 = M & 3, uA1 = M & 12, uB0 = M & 5, uB1 = M & 10;
+    accT acc[4];
 #pragma unroll
-  for (int s = 0; s < K2S; ++s) {
-    if (!live[s]) continue;
+    for (int t = 0; t < 4; ++t) acc[t] = accT{0, 0, 0, 0};
+    auto mfma_chunk = [&](const T* cur) {
+#pragma unroll
+      for (int kk = 0; kk < KC; kk += 4) {
+        T x[4] = {0, 0, 0, 0};
+        if constexpr (uA0) x[0] = cur[foff[0] + kk * STRIDE];
+        if constexpr (uA1) x[1] = cur[foff[1] + kk * STRIDE];
+        if constexpr (uB0) x[2] = cur[foff[2] + kk * STRIDE];
+        if constexpr (uB1) x[3] = cur[foff[3] + kk * STRIDE];
+        auto tile = [&](auto tc) {  // tile t = 2a + b: A fragment a, B fragment 2 + b
+          constexpr int t = decltype(tc)::value;
+          if constexpr (((M >> t) & 1) != 0) {
+            if constexpr (sizeof(T) == 8)
+              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[t >> 1], x[2 + (t & 1)], acc[t], 0, 0, 0);
+            else
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[t >> 1], x[2 + (t & 1)], acc[t], 0, 0, 0);
+          }
+        };
+        tile(std::integral_constant<int, 0>{});
+        tile(std::integral_constant<int, 1>{});
+        tile(std::integral_constant<int, 2>{});
+        tile(std::integral_constant<int, 3>{});
+      }
+    };
+    constexpr std::integral_constant<int, 0> A{};
+    constexpr std::integral_constant<int, 1> B{};
+    __syncthreads();  // LDS zeroed
+    if (nfull > 0) {
+      load_full(0, A);
+      load_full(1, B);
+      store_set(A, lds);
+    }
+    __syncthreads();
+    int64_t c = 0;
+    for (; c + 1 < nfull; c += 2) {  // chunks c (buffer 0, set A) and c + 1 (buffer 1, set B)
+      load_full(c + 2, A);
+      mfma_chunk(lds);
+      store_set(B, lds + BUF);
+      __syncthreads();
+      load_full(c + 3, B);
+      mfma_chunk(lds + BUF);
+      if (c + 2 < nfull) store_set(A, lds);
+      __syncthreads();
+    }
+    if (c < nfull) {  // an odd last full chunk, already in buffer 0
+      mfma_chunk(lds);
+      __syncthreads();
+    }
+    if (r0 + nfull * KC < r1) {  // the panel's partial last chunk
+      load_chunk(r0 + nfull * KC);
+      store_chunk(lds);
+      __syncthreads();
+      mfma_chunk(lds);
+    }
+    // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
+    if (!live) return;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      double* o = slab + ((size_t)ks * nslots + (size_t)(sbase + s) * 4 + t) * 256;
+      double* o = slab + ((size_t)ks * nslots + (size_t)sbase * 4 + t) * 256;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = sizeof(T) == 8 ? (lane >> 4) + 4 * j : 4 * (lane >> 4) + j;
         double* x = o + row * 16 + (lane & 15);
-        const double v = (double)acc[s][t][j];
+        const double v = (double)acc[t][j];
         *x = accumulate ? *x + v : v;  // chunked Gram: slabs carry over chunks
       }
     }
-  }
-  if constexpr (NVS > 0) {
-    // structured tiles (I, J), J in [ntm, NTC), I <= J: lane r writes row r % 16 of tile (r / 16, J), its
-    // B_c / tau entries and zeros (wave-uniform column positions)
-    if (sw && sr < 16 * NTC) {
-      const int I = sr >> 4, rr = sr & 15;
-      int slot = sx.slot0;
-      for (int J = ntm; J < NTC; ++J) {
-        if (I <= J) {
-          double* o = slab + ((size_t)ks * nslots + (size_t)(slot + I)) * 256 + rr * 16;
-#pragma unroll
-          for (int x = 0; x < 16; ++x) {
-            const int jb = 16 * J + x - sx.bc0;  // B_c joint of column 16 J + x (tau: jb == NJS)
-            double w = jb == NJS ? stau : 0.0;
-#pragma unroll
-            for (int j = JS0; j < NJS; ++j) w = jb == j ? sbc[j - JS0] : w;
-            o[x] = accumulate ? o[x] + w : w;
-          }
-        }
-        slot += J + 1;
-      }
-    }
+  };
+  switch (mask) {
+#define SYSID_K2_MASK(m) \
+  case m:                \
+    run(std::integral_constant<int, m>{}); \
+    break;
+    SYSID_K2_MASK(0) SYSID_K2_MASK(1) SYSID_K2_MASK(2) SYSID_K2_MASK(3) SYSID_K2_MASK(4) SYSID_K2_MASK(5)
+    SYSID_K2_MASK(6) SYSID_K2_MASK(7) SYSID_K2_MASK(8) SYSID_K2_MASK(9) SYSID_K2_MASK(10) SYSID_K2_MASK(11)
+    SYSID_K2_MASK(12) SYSID_K2_MASK(13) SYSID_K2_MASK(14) SYSID_K2_MASK(15)
+#undef SYSID_K2_MASK
   }
 }
 
@@ -3080,8 +3003,8 @@ k3_gram_reduce(const double* __restrict__ slab, const int2* __restrict__ tiles, 
   if (wave == 0) {
     const int x = (int)(e & 255);
     const int gi = ij.x * 16 + (x >> 4), gj = ij.y * 16 + (x & 15);
-    // a diagonal tile's upper half only: its two halves may differ by rounding (the structured tiles of
-    // k2_gram_syrk NVS > 0), and both entries write both mirrored positions
+    // a diagonal tile's upper half only, each entry written to both mirrored positions: the Gram is bitwise
+    // symmetric whatever order the MFMA summed a diagonal tile's two halves in
     if (gi < ncol && gj < ncol && (ij.x != ij.y || (x >> 4) <= (x & 15))) {
       const double acc = red[0][lane];
       G[(int64_t)gi * ncol + gj] = acc;

@@ -46,7 +46,6 @@ struct K2Args {
   hipStream_t st;
   const int* rowlist;
   const int* d_rows;
-  sysid_dev::K2Struct sx;  // structured B_c / tau columns (sx.in != nullptr; f64 narrow quadruped Grams)
 };
 // WIDE: Gram widths of 16..24 tile columns (else 1..15).  Returns false for a width outside the unit's range.
 template <int PREC, int WIDE>

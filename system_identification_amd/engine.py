@@ -383,8 +383,7 @@ class Engine:
         return list(cfg)
 
     def k2_config(self) -> list:
-        """K2 Gram deal [tile columns, MFMA tile columns of the structured f64 Gram (0: none), dense f64 tile slots,
-        structured tile slots]; SYSID_K2_STRUCT=0 at model creation selects the dense deal."""
+        """K2 Gram deal [tile columns, tile slots of the f64, f32 and bf16 deals]."""
         cfg = (ctypes.c_int32 * 4)()
         self._check(self.lib.sysid_debug_k2_config(self._h, cfg))
         return list(cfg)

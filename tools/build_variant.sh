@@ -1,6 +1,13 @@
 #!/bin/bash
 # Build a library variant with extra defines: bash tools/build_variant.sh <out.so> [-DFOO=1 ...]
-out=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -Isystem_identification_amd/csrc "$@" \
-  -o $out system_identification_amd/csrc/sysid_engine.hip system_identification_amd/csrc/sysid_io.cpp \
-  system_identification_amd/csrc/sysid_rccl.cpp -lpthread -ldl
+set -e
+out=$(realpath -m $1); shift
+tmp=$(mktemp -d)
+python3 - "$out" "$tmp" "$@" <<'PY'
+import sys
+sys.path.insert(0, ".")
+import __graft_entry__ as g
+out, tmp, extra = sys.argv[1], sys.argv[2], sys.argv[3:]
+g.build_library(out=out, obj_dir=tmp + "/obj", extra=extra, force=True)
+PY
+rm -rf $tmp
