@@ -372,6 +372,18 @@ __device__ __forceinline__ void panel_store(__bf16* p, double a, double b) {
   v[1] = (__bf16)fb;
   *reinterpret_cast<bf16x2_t*>(p) = v;
 }
+// bf16 store of two f32 values (the f32 row loop of the Q-form, below): one RNE conversion each
+__device__ __forceinline__ void panel_store_f32(__bf16* p, float a, float b) {
+  bf16x2_t v;
+  v[0] = (__bf16)a;
+  v[1] = (__bf16)b;
+  *reinterpret_cast<bf16x2_t*>(p) = v;
+}
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// v of the partner lane (lane ^ 1), f32
+__device__ __forceinline__ float pair_swap_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
 
 
 // Columns 0..3 (m, mc) of the block: F[6c .. 6c+5] = [linear; angular] of column c.
@@ -1514,8 +1526,66 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
             if (h) panel_store(o2 + 4, y[4], y[5]);
           }
         };
-        if (kq <= 3) rows(std::integral_constant<int, 3>{});
-        else rows(std::integral_constant<int, K1_QF_KMAX>{});
+        // bf16 chunk panels (the Gram-only bf16 Gram, config 5): the same row loop in f32 with packed FMAs
+        // (v_pk_fma_f32: two FMAs per instruction at the cost of one f64 FMA).  G and the block's outputs carry
+        // ~1e-7 relative error, far below the bf16 rounding (2^-9) the panel gets anyway; K and F6 are formed in
+        // f64 and rounded once.
+        auto rows_f32 = [&](auto kqc) {
+          constexpr int KQ = decltype(kqc)::value;
+          f32x2_t K01[KQ];
+          float K2[KQ];
+#pragma unroll
+          for (int j = 0; j < KQ; ++j) {
+            K01[j] = f32x2_t{(float)Kq[j][0], (float)Kq[j][1]};
+            K2[j] = (float)Kq[j][2];
+          }
+          f32x2_t Fp[3][6];  // Fp[p][q] = (F6[2p][q], F6[2p + 1][q])
+#pragma unroll
+          for (int pp = 0; pp < 3; ++pp)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) Fp[pp][q] = f32x2_t{(float)F6[2 * pp][q], (float)F6[2 * pp + 1][q]};
+#pragma unroll 1
+          for (int r = 0; r < nrows; ++r) {
+            const float sf = ((smask >> r) & 1ull) ? 1.0f : 0.0f;
+            const double* jr = jrs + 6 * r;
+            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
+            float qr[K1_QF_KMAX];
+#pragma unroll
+            for (int j = 0; j < (KQ + 1) / 2; ++j) {
+              const double2 v = q2[j];
+              qr[2 * j] = (float)v.x;
+              qr[2 * j + 1] = (float)v.y;
+            }
+            f32x2_t g01 = f32x2_t{sf * (float)jr[0], sf * (float)jr[1]};
+            float g2 = sf * (float)jr[2];
+#pragma unroll
+            for (int j = 0; j < KQ; ++j) {
+              g01 -= qr[j] * K01[j];
+              g2 -= qr[j] * K2[j];
+            }
+            const float G[6] = {g01.x, g01.y, g2, pair_swap_f32(g01.x), pair_swap_f32(g01.y), pair_swap_f32(g2)};
+            f32x2_t y01 = f32x2_t{0.0f, 0.0f}, y23 = y01, y45 = y01;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+              y01 += G[q] * Fp[0][q];
+              y23 += G[q] * Fp[1][q];
+            }
+            // outputs 4, 5: h = 1 lanes only, whose slots 3..5 are zero
+#pragma unroll
+            for (int q = 0; q < 3; ++q) y45 += G[q] * Fp[2][q];
+            __bf16* o2 = reinterpret_cast<__bf16*>(oi + (int64_t)r * ldp);
+            panel_store_f32(o2, y01.x, y01.y);
+            panel_store_f32(o2 + 2, y23.x, y23.y);
+            if (h) panel_store_f32(o2 + 4, y45.x, y45.y);
+          }
+        };
+        if constexpr (std::is_same_v<OutT, __bf16>) {
+          if (kq <= 3) rows_f32(std::integral_constant<int, 3>{});
+          else rows_f32(std::integral_constant<int, K1_QF_KMAX>{});
+        } else {
+          if (kq <= 3) rows(std::integral_constant<int, 3>{});
+          else rows(std::integral_constant<int, K1_QF_KMAX>{});
+        }
       }
     } else {
       for (int it = hl; it < nyi && valid; it += HW) {
@@ -1935,19 +2005,26 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
       __syncthreads();
       mfma_chunk(lds);
     }
-    // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32
+    // D layout: col = lane & 15; row = (lane >> 4) + 4 * reg for f64, 4 * (lane >> 4) + reg for f32.  Only the
+    // mask's tiles are written: K3 reads the tile slots the deal lists, never a skipped one.
     if (!live) return;
+    auto put = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (((M >> t) & 1) != 0) {
+        double* o = slab + ((size_t)ks * nslots + (size_t)sbase * 4 + t) * 256;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      double* o = slab + ((size_t)ks * nslots + (size_t)sbase * 4 + t) * 256;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = sizeof(T) == 8 ? (lane >> 4) + 4 * j : 4 * (lane >> 4) + j;
-        double* x = o + row * 16 + (lane & 15);
-        const double v = (double)acc[t][j];
-        *x = accumulate ? *x + v : v;  // chunked Gram: slabs carry over chunks
+        for (int j = 0; j < 4; ++j) {
+          const int row = sizeof(T) == 8 ? (lane >> 4) + 4 * j : 4 * (lane >> 4) + j;
+          double* x = o + row * 16 + (lane & 15);
+          const double v = (double)acc[t][j];
+          *x = accumulate ? *x + v : v;  // chunked Gram: slabs carry over chunks
+        }
       }
-    }
+    };
+    put(std::integral_constant<int, 0>{});
+    put(std::integral_constant<int, 1>{});
+    put(std::integral_constant<int, 2>{});
+    put(std::integral_constant<int, 3>{});
   };
   switch (mask) {
 #define SYSID_K2_MASK(m) \

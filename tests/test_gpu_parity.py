@@ -343,7 +343,9 @@ def test_reduced_precision_gram_matches_rounded_panel(robot, N):
     """The f32 / bf16 Gram kernels (each with its own super-tile deal and K3 reduction) against the exact
     Gram of the panel rounded the way K1 rounds it (f64 -> f32, then -> bf16, both RNE): what remains is only
     the kernels' f32 accumulation, so the bound is tight (1e-5 normwise), unlike the error against the f64
-    Gram that test_reduced_precision_gram reports.  Gram-only output from the reference's P·A rows (the
+    Gram that test_reduced_precision_gram reports.  (The Q-form models' bf16 rows come from K1's f32 row loop,
+    ~1e-7 relative before the bf16 rounding: an entry near a rounding boundary may land one bf16 ulp away,
+    far inside the bound.)  Gram-only output from the reference's P·A rows (the
     GRAM_PROJECTOR rows, the same rows the full path's f64 panel holds) vs that panel."""
     import torch
     model = load_robot(robot)
