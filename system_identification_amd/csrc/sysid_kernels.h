@@ -2870,13 +2870,59 @@ __device__ __forceinline__ void k2x_mfma(const T* cur, int lb, typename K2Acc<T>
     if constexpr (sizeof(T) == 8) return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
     else return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   };
+  if constexpr (sizeof(T) == 8) {
+    // f64: fragments read next to their MFMAs (the 64-cycle MFMAs cover the reads; the f32 form below measured
+    // 1.1% slower here, profiles/r03_n)
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      const T* base = cur + kk * STRIDE + lb;
+      if constexpr (R.diag) {
+        T f[R.nr];
+#pragma unroll
+        for (int i = 0; i < R.nr; ++i) f[i] = base[16 * (R.ra + i)];
+#pragma unroll
+        for (int i = 0; i < R.nr; ++i)
+#pragma unroll
+          for (int j = i; j < R.nr; ++j) {
+            const int x = i * R.nr - i * (i - 1) / 2 + (j - i);
+            acc[x] = mm(f[i], f[j], acc[x]);
+          }
+      } else {
+        T a[R.nr];
+#pragma unroll
+        for (int i = 0; i < R.nr; ++i) a[i] = base[16 * (R.ra + i)];
+#pragma unroll
+        for (int j = 0; j < R.nc; ++j) {
+          const T b = base[16 * (R.ca + j)];
+#pragma unroll
+          for (int i = 0; i < R.nr; ++i) acc[i * R.nc + j] = mm(a[i], b, acc[i * R.nc + j]);
+        }
+      }
+    }
+    return;
+  }
+  // f32: every fragment of k-step kk + 4 is read before k-step kk's MFMAs issue (two register sets, renamed by the
+  // unrolled loop): the reads of one k-step land while the previous one multiplies.  Reading each column block's
+  // fragment just before its MFMAs (the compiler's own schedule) left an lgkmcnt(0) wait in front of every group
+  // of nr MFMAs (361 in the G1 kernel, 90 after), with only two waves per SIMD to hide it: G1 125k f32 K2 -3.4%.
+  constexpr int NF = R.diag ? R.nr : R.nr + R.nc;
+  auto load = [&](int kk, T (&f)[NF]) {
+    const T* base = cur + kk * STRIDE + lb;
+#pragma unroll
+    for (int i = 0; i < R.nr; ++i) f[i] = base[16 * (R.ra + i)];
+    if constexpr (!R.diag) {
+#pragma unroll
+      for (int j = 0; j < R.nc; ++j) f[R.nr + j] = base[16 * (R.ca + j)];
+    }
+  };
+  T f[NF];
+  load(0, f);
 #pragma unroll
   for (int kk = 0; kk < KC; kk += 4) {
-    const T* base = cur + kk * STRIDE + lb;
+    T g[NF];
+    if (kk + 4 < KC) load(kk + 4, g);
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this k-step's MFMAs (the scheduler sinks them)
     if constexpr (R.diag) {
-      T f[R.nr];
-#pragma unroll
-      for (int i = 0; i < R.nr; ++i) f[i] = base[16 * (R.ra + i)];
 #pragma unroll
       for (int i = 0; i < R.nr; ++i)
 #pragma unroll
@@ -2885,15 +2931,14 @@ __device__ __forceinline__ void k2x_mfma(const T* cur, int lb, typename K2Acc<T>
           acc[x] = mm(f[i], f[j], acc[x]);
         }
     } else {
-      T a[R.nr];
 #pragma unroll
-      for (int i = 0; i < R.nr; ++i) a[i] = base[16 * (R.ra + i)];
+      for (int j = 0; j < R.nc; ++j)
 #pragma unroll
-      for (int j = 0; j < R.nc; ++j) {
-        const T b = base[16 * (R.ca + j)];
+        for (int i = 0; i < R.nr; ++i) acc[i * R.nc + j] = mm(f[i], f[R.nr + j], acc[i * R.nc + j]);
+    }
+    if (kk + 4 < KC) {
 #pragma unroll
-        for (int i = 0; i < R.nr; ++i) acc[i * R.nc + j] = mm(a[i], b, acc[i * R.nc + j]);
-      }
+      for (int i = 0; i < NF; ++i) f[i] = g[i];
     }
   }
 }
