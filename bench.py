@@ -76,8 +76,8 @@ def pmc_traffic(kernel, robot, samples):
     import glob
     import re
 
-    def version(path):  # r01_v10 sorts after r01_v9: compare the numbers, not the strings
-        return [int(n) for n in re.findall(r"\d+", os.path.basename(os.path.dirname(path)))]
+    def version(path):  # r01_v10 after r01_v9 (numbers as numbers), r03_p after r03_m (round, then the tag)
+        return [int(t) if t.isdigit() else t for t in re.findall(r"\d+|[a-z]+", os.path.basename(os.path.dirname(path)))]
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), key=version, reverse=True):
         try:

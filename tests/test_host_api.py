@@ -201,3 +201,27 @@ def test_gram_llsq_noise_floor_is_pinned():
     cs, cg = V.T @ phi_s, V.T @ phi_g
     assert abs(cs[-2] - 1.0) < 1e-6 and abs(cg[-2] - 1.0) < 1e-3   # sigma = 1e-5 sigma_max: both
     assert abs(cs[-1] - 1.0) < 1e-3 and abs(cg[-1]) < 1e-6          # sigma = 1e-8: stacked only
+
+
+def test_bench_traffic_source_is_the_newest_profile(tmp_path, monkeypatch):
+    """bench.py's roofline `traffic` comes from the newest committed PMC summary of the same workload:
+    r01_v10 after r01_v9 (numbers compared as numbers), r03_p after r03_m (same round: the later tag)."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for name, fetch in [("r01_v9", 1.0), ("r01_v10", 2.0), ("r03_m", 3.0), ("r03_p", 4.0), ("r02_v9", 5.0)]:
+        d = tmp_path / "profiles" / name
+        d.mkdir(parents=True)
+        (d / "pmc_summary.json").write_text(json.dumps({
+            "_config": {"robot": "spot", "samples": 20000},
+            "k2_gram_syrk": {"FETCH_bytes_corrected_x2": fetch, "WRITE_bytes": 0.0}}))
+    other = tmp_path / "profiles" / "r03_q"
+    other.mkdir()
+    (other / "pmc_summary.json").write_text(json.dumps({"_config": {"robot": "g1_29dof", "samples": 20000},
+                                                        "k2_gram_syrk": {"FETCH_bytes_corrected_x2": 9.0,
+                                                                         "WRITE_bytes": 0.0}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    traffic, src = bench.pmc_traffic("k2_gram_syrk", "spot", 20000)
+    assert src.endswith(os.path.join("r03_p", "pmc_summary.json")) and traffic == 4
