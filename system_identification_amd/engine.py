@@ -56,6 +56,7 @@ SIGNATURES = [
     ("sysid_debug_layout", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_debug_k1_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_gram_rows", _c.c_int32, [_vp, _c.c_uint32]),
+    ("sysid_set_gram_chunk_bytes", _c.c_int32, [_vp, _c.c_uint64]),
     ("sysid_debug_k2_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
@@ -369,6 +370,11 @@ class Engine:
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)
+
+    def set_gram_chunk_bytes(self, nbytes: int) -> None:
+        """Chunk panel size of the Gram-only path (>= 1 MiB; 0 = the 4 GiB default).  alloc_gram_device /
+        gram_workspace_bytes follow it, so set it before allocating."""
+        self._check(self.lib.sysid_set_gram_chunk_bytes(self._h, int(nbytes)))
 
     def gram_rows(self, precision: str = "f64", rows: str = "auto") -> str:
         """The rows build_gram_device uses: "nullspace" (Zᵀ·A) or "projector" (P·A)."""

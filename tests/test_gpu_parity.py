@@ -254,11 +254,13 @@ def test_hip_graph_replay_matches_eager(robot, N):
 
 @pytest.mark.parametrize("robot,N", [("spot", 50000), ("g1_29dof", 12000)])
 def test_gram_only_chunked(robot, N):
-    """Gram-only path (panel produced in ~1 GiB chunks on the device, several chunks here) against
-    the full-panel path, on the host API and on the device API; bitwise repeatable."""
+    """Gram-only path (the panel produced in chunks on the device: 256 MiB chunks here, 5 of them) against
+    the full-panel path, on the host API and on the device API; bitwise repeatable; the default 4 GiB chunk
+    (one chunk here) gives the same Gram to rounding."""
     import torch
     model = load_robot(robot)
-    e = eng(robot)
+    e = Engine(model)
+    e.set_gram_chunk_bytes(256 << 20)
     d = generate(model, N, config_index=3)
     full = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_ALL)
     only = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_GRAM)
@@ -279,6 +281,10 @@ def test_gram_only_chunked(robot, N):
     small = {"gram": bufs["gram"], "ws": bufs["ws"][:1024]}
     with pytest.raises(ValueError):
         e.build_gram_device(din, N, small)
+    one = eng(robot).build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_GRAM)
+    assert rel(one["gram"], only["gram"]) < 1e-12
+    with pytest.raises(ValueError):
+        e.set_gram_chunk_bytes(1000)
 
 
 @pytest.mark.parametrize("robot,N", [("spot", 3000), ("g1_29dof", 700)])
