@@ -32,8 +32,11 @@ i = k.index(anchor)
 j = k.index("    wsync();\n", i)
 k = k[:j] + "    wsync();\n    K1STAMP(4)\n" + k[j + len("    wsync();\n"):]
 open("sysid_kernels.h", "w").write(k)
-e = open("sysid_engine.hip").read()
+# the readout lives in the translation unit of the f64 stacked-output K1 instantiations (sysid_k1_inst.hip with
+# SYSID_PREC=0, SYSID_CMP=0): every unit has its own copy of the __device__ accumulator
+e = open("sysid_k1_inst.hip").read()
 e += '''
+#if SYSID_PREC == 0 && SYSID_CMP == 0
 extern "C" int32_t sysid_debug_k1_stamps(unsigned long long* out10, int32_t reset) {
   if (reset) {
     unsigned long long z[16] = {0};
@@ -41,5 +44,6 @@ extern "C" int32_t sysid_debug_k1_stamps(unsigned long long* out10, int32_t rese
   }
   return hipMemcpyFromSymbol(out10, HIP_SYMBOL(sysid_dev::k1_stamp_sum), 10 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
 }
+#endif
 '''
-open("sysid_engine.hip", "w").write(e)
+open("sysid_k1_inst.hip", "w").write(e)
