@@ -47,7 +47,8 @@ def parse():
                     help="Gram arithmetic for --gram-only (f32/bf16: config 5 throughput, error reported)")
     ap.add_argument("--rows", default="auto", choices=["auto", "nullspace", "projector"],
                     help="--gram-only rows per sample: nullspace (nv - rank(J_c) rows Z^T A), projector (the "
-                         "reference's nv rows P A) or auto (nullspace for f64/f32 Grams, projector for bf16)")
+                         "reference's nv rows P A) or auto (the engine's choice, Engine.gram_rows: nullspace unless the "
+                         "model runs the Q-form K1 (G1, snake14) or the Gram is bf16; the JSON names it as rows_used)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) legs")
     ap.add_argument("--graph", action="store_true",
@@ -64,9 +65,12 @@ def parse():
     ap.add_argument("--exchange-world1", action="store_true",
                     help="test mode: run the C-ABI RCCL exchange on a one-rank communicator at N = 1, so the "
                          "(overlapped) exchange path runs on a single GPU; not a driver configuration")
-    ap.add_argument("--settle-ms", type=float, default=250.0,
-                    help="untimed steps run back to back for at least this long before the warmup steps, so the "
-                         "GPU's clocks reach their operating point (0 = off); reported as `settle` in the JSON")
+    ap.add_argument("--settle-ms", type=float, default=0.0,
+                    help="untimed steps run back to back for at least this long before the warmup steps (0 = off, "
+                         "the default: the timed region follows exactly --warmup steps).  The steady-state figure "
+                         "after a 250 ms settle is reported separately as `steady_state` (N = 1), never as `value`")
+    ap.add_argument("--no-steady-state", action="store_true",
+                    help="skip the labelled steady-state re-timing after the timed region")
     return ap.parse_args()
 
 
@@ -77,7 +81,9 @@ def pmc_traffic(kernel, robot, samples):
     import re
 
     def version(path):  # r01_v10 after r01_v9 (numbers as numbers), r03_p after r03_m (round, then the tag)
-        return [int(t) if t.isdigit() else t for t in re.findall(r"\d+|[a-z]+", os.path.basename(os.path.dirname(path)))]
+        # type-stable key: numbers sort before words at the same position (r03_2 vs r03_j compares (0, 2) < (1, 'j'))
+        return [(0, int(t), "") if t.isdigit() else (1, 0, t)
+                for t in re.findall(r"\d+|[a-z]+", os.path.basename(os.path.dirname(path)))]
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), key=version, reverse=True):
         try:
@@ -223,6 +229,8 @@ def main():
             exchange_name = "sysid_allreduce_gram (RCCL, C ABI)"
 
     if args.gram_only:
+        # config 5: 16 GiB chunk panels (the library default is 4 GiB; 16 GiB measured 2-3% faster on G1 1M)
+        eng.set_gram_chunk_bytes(16 << 30)
         bufs = eng.alloc_gram_device(N)
 
         def launch(s, b=bufs):
@@ -287,27 +295,20 @@ def main():
             compute()
             exchange()
 
-    # The host-entry-point legs (their own measurement, SURVEY §8d's end-to-end rate; PCIe-inclusive, never the
-    # headline value) run here, before the warmup steps: ~40 ms of GPU work that brings the clocks to their
-    # operating point.  Run after the timed region instead, the driver's 5 warmup steps left the first timed steps
-    # ~15% slow (step_times first vs last quartile 0.406 vs 0.353 ms, profiles/r03_j/bench_driver.json).
-    # Nothing inside the timed region changes.
-    e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = e2e_legs(eng, data, N)
-        torch.cuda.synchronize()
-    # Clock settle (untimed, every rank): steps back to back until --settle-ms of wall time has passed.  The
-    # driver's 5 warmup steps are ~2 ms of Spot work; the clocks take longer than that to ramp (step_times of a
-    # 20-step run after 5 warmup steps: first-quartile mean 0.406 ms, last 0.353, steady state 0.318,
-    # profiles/r03_j).  Same launches as the timed steps minus the exchange (ranks may settle for different step
-    # counts, so no collective runs here); what is timed does not change.
-    settle_steps, t_settle = 0, time.perf_counter()
-    while args.settle_ms > 0 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-        for _ in range(8):
-            compute()
-        settle_steps += 8
-        torch.cuda.synchronize()
-    settle = {"steps": settle_steps, "ms": round((time.perf_counter() - t_settle) * 1e3, 1)}
+    # Optional clock settle (untimed, every rank; off by default): steps back to back until --settle-ms of wall
+    # time has passed.  By default the timed region follows exactly the --warmup steps the caller asked for, so a
+    # short run measures what a one-shot identification sees, clock ramp included (step_times shows it); the
+    # settled figure is re-measured after the timed region and reported apart (`steady_state`).
+    def settle_for(ms_budget):
+        n, t_s = 0, time.perf_counter()
+        while ms_budget > 0 and (time.perf_counter() - t_s) * 1e3 < ms_budget:
+            for _ in range(8):
+                compute()
+            n += 8
+            torch.cuda.synchronize()
+        return {"steps": n, "ms": round((time.perf_counter() - t_s) * 1e3, 1)}
+
+    settle = settle_for(args.settle_ms)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -330,6 +331,27 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # Labelled side figures, all after the timed region: the steady state (250 ms of untimed steps, then the same
+    # K steps re-timed; rank 0 at N = 1) and the host-entry-point legs (SURVEY §8d's end-to-end rate,
+    # PCIe-inclusive).  Neither is `value`.
+    steady = None
+    if world == 1 and not args.no_steady_state:
+        pre = settle_for(250.0)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            compute()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t1
+        steady = {"ms_per_step": round(el2 / args.steps * 1e3, 5),
+                  "samples_per_s": round(total_per_step * args.steps / el2, 1),
+                  "settle": pre, "note": "the same K steps re-timed after 250 ms of untimed back-to-back steps "
+                                         "(clocks at their operating point); not the headline value"}
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = e2e_legs(eng, data, N)
+        torch.cuda.synchronize()
 
     # Exchange check (after the timed region): every rank must hold the same reduced Gram in each buffer; with
     # the one-rank test communicator the all-reduce is the identity, so each buffer must equal a fresh local
@@ -418,6 +440,7 @@ def main():
                                                              else "")},
         "step_times": step_stats,
         "settle": settle,
+        "steady_state": steady,
         "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
         "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},

@@ -137,7 +137,7 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
                            void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Gram-only device entry point ("K1 fused with K2"): normal equations of N samples
- * without the N·nv-row panel.  The panel is produced in chunks (16 GiB by default) inside the workspace
+ * without the N·nv-row panel.  The panel is produced in chunks (4 GiB by default) inside the workspace
  * and folded into the same Gram accumulators chunk after chunk; d_gram as in sysid_build_device.
  * flags may select a reduced-precision Gram (SYSID_GRAM_F32 / SYSID_GRAM_BF16, config 5): K1 then writes
  * the chunk panel already rounded to f32 / bf16, and the Gram kernel runs on f32 / bf16 MFMA (f32
@@ -147,9 +147,13 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
 size_t sysid_gram_workspace_bytes(const sysid_engine* e, int64_t N);
 int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
                                 double* d_gram, void* d_workspace, size_t workspace_bytes, void* stream);
-/* Chunk panel size of the Gram-only path (bytes, >= 1 MiB; 0 restores the 16 GiB default): the workspace that
- * sysid_gram_workspace_bytes reports follows it.  Fewer, larger chunks are faster (each costs a K1 launch tail
- * and a pass over the split-K slabs); a smaller chunk bounds the device memory of very large N. */
+/* Chunk panel size of the Gram-only path (bytes, >= 1 MiB; 0 restores the 4 GiB default): the workspace that
+ * sysid_gram_workspace_bytes reports follows it.  That workspace is exactly: 1 KiB of K1 sample counters, the
+ * chunk panel (min(chunk bytes, N·nv rows of the Gram's element type)), the split-K slabs (K2 workgroups x
+ * Gram tile slots x 2 KiB: Spot <= 29 MB, G1 <= 141 MB) and, for the nullspace rows, 4·(nv + 1) bytes per
+ * chunk sample of row counts and row list plus 4 bytes per 1024 samples of segment sums.  Fewer, larger chunks
+ * are faster (each costs a K1 launch tail and a pass over the split-K slabs: 16 GiB is 2-3% faster than 4 GiB
+ * on G1 1M); a smaller chunk bounds the device memory of very large N. */
 int32_t sysid_set_gram_chunk_bytes(sysid_engine* e, uint64_t bytes);
 /* The rows sysid_build_gram_device uses for these flags: 1 = nullspace (Zᵀ·A), 0 = projector (P·A), < 0 error. */
 int32_t sysid_gram_rows(const sysid_engine* e, uint32_t flags);

@@ -42,7 +42,7 @@ constexpr size_t WORK_BYTES = 128 * K1_SHARDS;  // one 128-byte line per claim c
 
 struct sysid_engine {
   int device = 0;
-  size_t gram_chunk = (size_t)16 << 30;  // Gram-only chunk panel bytes (sysid_set_gram_chunk_bytes)
+  size_t gram_chunk = (size_t)4 << 30;  // Gram-only chunk panel bytes (sysid_set_gram_chunk_bytes)
   int cus = 256;
   hipStream_t stream = nullptr;
   int nq = 0, nv = 0, nj = 0, nb = 0, nc = 0, wy = 0, w = 0, ncol = 0, ldp = 0, in_rows = 0, in_lds = 0;
@@ -294,7 +294,8 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
 // Gram-only: the panel never leaves the device and is produced chunk by chunk into the workspace; K2
 // accumulates every chunk into the same slabs, K3 reduces once.  The chunk panel is in the Gram's arithmetic
 // (f64, or f32 / bf16 rounded by K1) with ld a multiple of 16 bytes' worth of elements.
-// Chunk panel of 16 GiB by default (sysid_set_gram_chunk_bytes): each chunk costs a K1 launch tail of partly idle
+// Chunk panel of 4 GiB by default (sysid_set_gram_chunk_bytes; bench.py's config-5 lines set 16 GiB, 2-3% faster
+// than 4 GiB): each chunk costs a K1 launch tail of partly idle
 // CUs and a K2 pass that reads and rewrites the split-K slabs (G1: 256 x 276 tiles x 2 KiB = 141 MB each way), so
 // few large chunks win and the MALL does not (G1 125k step, 128 MB / 256 MB / 1 GiB / 2 GiB / 4 GiB chunks: bf16
 // 6.39 / 4.45 / 3.25 / 3.05 / 2.82 ms, f32 12.1 / 10.6 / 7.62 / 7.17 / 7.00 ms; f64 1 -> 4 GiB 13.73 -> 12.98 ms;
@@ -1224,7 +1225,7 @@ int32_t sysid_set_gram_chunk_bytes(sysid_engine* e, uint64_t bytes) {
   if (bytes != 0 && bytes < ((uint64_t)1 << 20))
     return set_err(e, SYSID_E_INVALID, "Gram chunk of %llu bytes: at least 1 MiB (or 0 = the default)",
                    (unsigned long long)bytes);
-  e->gram_chunk = bytes ? (size_t)bytes : (size_t)16 << 30;
+  e->gram_chunk = bytes ? (size_t)bytes : (size_t)4 << 30;
   return SYSID_OK;
 }
 

@@ -372,7 +372,7 @@ class Engine:
         self._check(rc)
 
     def set_gram_chunk_bytes(self, nbytes: int) -> None:
-        """Chunk panel size of the Gram-only path (>= 1 MiB; 0 = the 16 GiB default).  alloc_gram_device /
+        """Chunk panel size of the Gram-only path (>= 1 MiB; 0 = the 4 GiB default).  alloc_gram_device /
         gram_workspace_bytes follow it, so set it before allocating."""
         self._check(self.lib.sysid_set_gram_chunk_bytes(self._h, int(nbytes)))
 

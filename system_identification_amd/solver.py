@@ -87,6 +87,10 @@ class Solver():
 
     # ------------ Constrained Solver (LMI) ------------ #
     def solve_fully_consistent(self, lambda_reg=1e-1, tol=1e-10, max_iters=1000, reg_type="constant_pullback"):
+        """solver.py:123-210.  ``reg_type`` is one of REG_TYPES; an unknown name raises ValueError (the reference
+        silently solves without a regulariser there, solver.py:161-180)."""
+        if reg_type not in REG_TYPES:
+            raise ValueError(f"unknown reg_type {reg_type!r}: expected one of {REG_TYPES}")
         try:
             import cvxpy as cp  # noqa: F401
         except ImportError as exc:  # pragma: no cover - depends on the host image
@@ -95,30 +99,109 @@ class Solver():
         return _solve_fully_consistent_cvxpy(self, lambda_reg, tol, max_iters, reg_type)
 
 
-def _pseudo_inertia(phi):
-    mass, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = phi
+REG_TYPES = ("constant_pullback", "entropic", "euclidean")
+
+
+# ---- per-link LMI matrices of the SDP (src/solver.py:42-121), numpy -----------------------------------------
+# phi = [m, h_x, h_y, h_z, I_xx, I_xy, I_xz, I_yy, I_yz, I_zz] (the order solver.py:44 / :55 unpack).  Every
+# matrix below is linear in phi, so the cvxpy path builds it as sum_k phi_k B_k from the basis these functions
+# give (lmi_basis): one definition serves the numeric checks and the SDP, and the coefficients CVXPY sees are
+# exactly the numbers the reference's hstack / vstack expressions carry.
+def spatial_body_inertia_matrix(phi):
+    """solver.py:42-51 — the 6x6 spatial body inertia [[I, h x]; [(h x)^T, m 1]] as the reference lays it out."""
+    m, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = np.asarray(phi, dtype=np.float64)
+    return np.array([[Ixx, Ixy, Ixz, 0.0, -hz, hy],
+                     [Ixy, Iyy, Iyz, hz, 0.0, -hx],
+                     [Ixz, Iyz, Izz, -hy, hx, 0.0],
+                     [0.0, hz, -hy, m, 0.0, 0.0],
+                     [-hz, 0.0, hx, 0.0, m, 0.0],
+                     [hy, -hx, 0.0, 0.0, 0.0, m]])
+
+
+def pseudo_inertia_matrix(phi):
+    """solver.py:53-63 — J (4x4): [[tr/2 - I_xx, -I_xy, -I_xz, h_x], ..., [h_x, h_y, h_z, m]], tr = I_xx+I_yy+I_zz."""
+    m, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = np.asarray(phi, dtype=np.float64)
     tr = 0.5 * (Ixx + Iyy + Izz)
-    return np.array([[tr - Ixx, -Ixy, -Ixz, hx], [-Ixy, tr - Iyy, -Iyz, hy], [-Ixz, -Iyz, tr - Izz, hz],
-                     [hx, hy, hz, mass]])
+    return np.array([[tr - Ixx, -Ixy, -Ixz, hx],
+                     [-Ixy, tr - Iyy, -Iyz, hy],
+                     [-Ixz, -Iyz, tr - Izz, hz],
+                     [hx, hy, hz, m]])
+
+
+def ellipsoid_matrix(semi_axes, center):
+    """solver.py:65-74 — Q_full (4x4) of the bounding ellipsoid, stored in float32 as the reference stores it
+    (the products are formed in the inputs' precision, then rounded once into the float32 matrix)."""
+    semi_axes, center = np.asarray(semi_axes), np.asarray(center)
+    Q_full = np.zeros((4, 4), dtype=np.float32)
+    Q = np.linalg.inv(np.diag(semi_axes) ** 2)
+    Q_full[:3, :3] = Q
+    Q_full[:3, 3] = Q @ center
+    Q_full[3, :3] = (Q @ center).T
+    Q_full[3, 3] = 1 - (center.T @ Q @ center)
+    return Q_full
+
+
+def com_constraint_matrix(phi, semi_axes, center):
+    """solver.py:76-93 — [[m, (h - m c)^T]; [h - m c, m diag(semi_axes)^2]]."""
+    phi = np.asarray(phi, dtype=np.float64)
+    m, h = phi[0], phi[1:4]
+    Qs = np.diag(np.asarray(semi_axes)) ** 2
+    top = (h - m * np.asarray(center)).reshape(1, 3)
+    return np.block([[np.array([[m]]), top], [top.T, m * Qs]])
+
+
+def lmi_basis(fn, *args):
+    """B[k] = fn(e_k, *args) for the 10 unit vectors: fn(phi, *args) == sum_k phi_k B[k] for a linear fn."""
+    return np.stack([fn(np.eye(10)[k], *args) for k in range(10)])
 
 
 def pullback_metric(phi_prior_link):
     """solver.py:95-121 — constant pull-back approximation of the Riemannian metric at the prior."""
     M = np.zeros((10, 10))
-    P_inv = np.linalg.inv(_pseudo_inertia(phi_prior_link))
+    P_inv = np.linalg.inv(pseudo_inertia_matrix(phi_prior_link))
     for i in range(10):
         for j in range(10):
             vi = np.zeros(10)
             vj = np.zeros(10)
             vi[i] = 1
             vj[j] = 1
-            M[i, j] = np.trace(P_inv @ _pseudo_inertia(vi) @ P_inv @ _pseudo_inertia(vj))
+            M[i, j] = np.trace(P_inv @ pseudo_inertia_matrix(vi) @ P_inv @ pseudo_inertia_matrix(vj))
     M = (M + M.T) / 2
     ev = np.linalg.eigvals(M)
     if np.any(ev < 0):
         M = M + (-np.min(ev) + 1e-5) * np.eye(10)
     assert np.min(np.linalg.eigvals(M)) > 0
     return M
+
+
+def entropic_prior_terms(phi_prior_link):
+    """solver.py:164-172 — the constants of the entropic (log-det Bregman) term at the prior: X_map with
+    X = X_map @ J (the SVD pseudo-inverse of J_prior, VT.T @ pinv(diag(Sigma)) @ U.T) and log(det(J_prior) + 1e-5)."""
+    J_prior = pseudo_inertia_matrix(phi_prior_link)
+    U, Sigma, VT = np.linalg.svd(J_prior, full_matrices=True)
+    Sigma_inv = np.linalg.pinv(np.diag(Sigma))
+    return VT.T @ Sigma_inv @ U.T, float(np.log(np.linalg.det(J_prior) + 1e-5))
+
+
+def entropic_divergence(phi_link, phi_prior_link):
+    """The value of the reference's entropic regulariser for one link at a numeric phi (solver.py:172):
+    -log det J + log(det J_prior + 1e-5) + trace(X) - 4, X = pinv_svd(J_prior) J."""
+    X_map, log_det_prior = entropic_prior_terms(phi_prior_link)
+    J = pseudo_inertia_matrix(phi_link)
+    sign, logdet = np.linalg.slogdet(J)
+    if sign <= 0:
+        return np.inf
+    return -logdet + log_det_prior + float(np.trace(X_map @ J)) - 4.0
+
+
+def link_lmi_values(phi_link, semi_axes, center, epsilon=1e-6):
+    """The constraint matrices of one link as solve_fully_consistent states them (solver.py:139-157), at a
+    numeric phi: J + eps I (>> 0), com + eps I (>> 0), trace(J Q_full) (>= 0), mass (>= 0)."""
+    J = pseudo_inertia_matrix(phi_link)
+    return {"J_reg": J + epsilon * np.eye(4),
+            "com_reg": com_constraint_matrix(phi_link, semi_axes, center) + epsilon * np.eye(4),
+            "trace_JQ": float(np.trace(J @ ellipsoid_matrix(semi_axes, center))),
+            "mass": float(np.asarray(phi_link)[0])}
 
 
 def gram_data_term(G, g, btb):
@@ -138,39 +221,44 @@ def gram_data_value(R, g, btb, x):
     return float(Rx @ Rx - 2.0 * (g @ x) + btb)
 
 
-def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_type):  # pragma: no cover
+def _affine(cp, p, basis):
+    """sum_k p[k] basis[k] as a CVXPY expression (basis: (10, r, c) constants): vec_F of the matrix is
+    basis_F @ p, reshaped column-major (CVXPY's default order)."""
+    r, c = basis.shape[1:]
+    Bf = np.stack([basis[k].reshape(-1, order="F") for k in range(10)], axis=1)  # (r c, 10)
+    return cp.reshape(Bf @ p, (r, c), order="F")
+
+
+def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_type):
+    """solver.py:123-210 with the LMI matrices from the numpy functions above (lmi_basis); the data term from the
+    stacked arrays (reference form) or from the normal equations (gram_data_term)."""
     import cvxpy as cp
     nx = s._nx
     phi = cp.Variable(nx, value=np.asarray(s._phi_prior, dtype=float))
     cons = []
     reg = 0
     mass_sum = 0
+    eps = 1e-6
+    PI = lmi_basis(pseudo_inertia_matrix)
     for idx in range(s._num_links):
-        j = idx * 10
-        p = phi[j:j + 10]
-        prior = np.asarray(s._phi_prior[j:j + 10], dtype=float)
+        j = idx * s._num_inertial_params
+        p = phi[j:j + s._num_inertial_params]
+        prior = np.asarray(s._phi_prior[j:j + s._num_inertial_params], dtype=float)
         ell = s._bounding_ellipsoids[idx]
         semi, center = np.asarray(ell["semi_axes"]), np.asarray(ell["center"])
         cons.append(p[0] >= 0)
         mass_sum += p[0]
-        m, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = [p[k] for k in range(10)]
-        tr = 0.5 * (Ixx + Iyy + Izz)
-        J = cp.vstack([cp.hstack([tr - Ixx, -Ixy, -Ixz, hx]), cp.hstack([-Ixy, tr - Iyy, -Iyz, hy]),
-                       cp.hstack([-Ixz, -Iyz, tr - Izz, hz]), cp.hstack([hx, hy, hz, m])])
-        cons.append(J + 1e-6 * np.eye(4) >> 0)
-        Qs = np.diag(semi) ** 2
-        tr_ = cp.reshape(p[1:4] - p[0] * center, (1, 3))
-        com = cp.bmat([[cp.reshape(p[0], (1, 1)), tr_], [tr_.T, p[0] * Qs]])
-        cons.append(com + 1e-6 * np.eye(4) >> 0)
-        Q = np.linalg.inv(np.diag(semi) ** 2)
-        Qf = np.zeros((4, 4))
-        Qf[:3, :3] = Q
-        Qf[:3, 3] = Q @ center
-        Qf[3, :3] = Q @ center
-        Qf[3, 3] = 1 - center @ Q @ center
-        cons.append(cp.trace(J @ Qf) >= 0)
+        J = _affine(cp, p, PI)
+        cons.append(J + eps * cp.Constant(np.eye(4)) >> 0)
+        com = _affine(cp, p, lmi_basis(com_constraint_matrix, semi, center))
+        cons.append(com + eps * cp.Constant(np.eye(4)) >> 0)
+        cons.append(cp.trace(J @ ellipsoid_matrix(semi, center)) >= 0)
         if reg_type == "constant_pullback":
             reg += 0.5 * cp.quad_form(p - prior, pullback_metric(prior))
+        elif reg_type == "entropic":
+            # solver.py:164-172 (the reference notes that this form may not converge)
+            X_map, log_det_prior = entropic_prior_terms(prior)
+            reg += -cp.log_det(J) + log_det_prior + cp.trace(X_map @ J) - 4
     if reg_type == "euclidean":
         reg = cp.quad_form(phi - np.asarray(s._phi_prior, dtype=float), np.eye(nx))
     cons.append(mass_sum == s.total_mass)
@@ -192,13 +280,19 @@ def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_typ
             G, g = G[:nx, :nx], g[:nx]
         R, g, btb = gram_data_term(G, g, btb)
         err = cp.sum_squares(R @ x) - 2 * g @ x + btb
-    prob = cp.Problem(cp.Minimize(0.5 * err / s._num_samples + lambda_reg * reg), cons)
-    prob.solve(solver=cp.MOSEK, mosek_params={"MSK_IPAR_INTPNT_SOLVE_FORM": "MSK_SOLVE_PRIMAL",
-                                              "MSK_DPAR_INTPNT_TOL_REL_GAP": tol,
-                                              "MSK_DPAR_OPTIMIZER_MAX_TIME": 100.0,
-                                              "MSK_IPAR_INTPNT_MAX_ITERATIONS": max_iters}, verbose=True)
-    if prob.status in (cp.OPTIMAL, cp.OPTIMAL_INACCURATE):
+    s._constraints = cons
+    s._objective = cp.Minimize(0.5 * err / s._num_samples + lambda_reg * reg)
+    s._problem = cp.Problem(s._objective, cons)
+    try:
+        s._problem.solve(solver=cp.MOSEK, mosek_params={"MSK_IPAR_INTPNT_SOLVE_FORM": "MSK_SOLVE_PRIMAL",
+                                                         "MSK_DPAR_INTPNT_TOL_REL_GAP": tol,
+                                                         "MSK_DPAR_OPTIMIZER_MAX_TIME": 100.0,
+                                                         "MSK_IPAR_INTPNT_MAX_ITERATIONS": max_iters}, verbose=True)
+    except Exception as e:  # noqa: BLE001 - solver.py:200-201 prints and falls through to the status check
+        print(e)
+    if s._problem.status in (cp.OPTIMAL, cp.OPTIMAL_INACCURATE):
         return phi.value
+    print("The problem did not solve to optimality. Status:", s._problem.status)
     raise ValueError("The problem did not solve to optimality.")
 
 

@@ -15,6 +15,7 @@ import numpy as np
 
 from . import engine as _engine
 from .model import Model, build_model_from_urdf, load_robot, rpy_to_matrix, skew
+from .solver import ellipsoid_matrix
 
 
 def _resolve_model(urdf_file, config_file, floating_base) -> Model:
@@ -205,12 +206,7 @@ class SystemIdentification(object):
             J[:3, 3] = h
             J[3, :3] = h
             J[3, 3] = m
-            Qf = np.zeros((4, 4), dtype=np.float32)
-            Q = np.linalg.inv(np.diag(semi) ** 2)
-            Qf[:3, :3] = Q
-            Qf[:3, 3] = Q @ center
-            Qf[3, :3] = Q @ center
-            Qf[3, 3] = 1 - center @ Q @ center
+            Qf = ellipsoid_matrix(semi, center)  # float32, as solver.py:65-74 and :360-366 build it
             C = np.zeros((4, 4), dtype=np.float32)
             C[0, 0] = m
             C[0, 1:] = h - m * center

@@ -255,7 +255,7 @@ def test_hip_graph_replay_matches_eager(robot, N):
 @pytest.mark.parametrize("robot,N", [("spot", 50000), ("g1_29dof", 12000)])
 def test_gram_only_chunked(robot, N):
     """Gram-only path (the panel produced in chunks on the device: 256 MiB chunks here, 5 of them) against
-    the full-panel path, on the host API and on the device API; bitwise repeatable; the default 16 GiB chunk
+    the full-panel path, on the host API and on the device API; bitwise repeatable; the default 4 GiB chunk
     (one chunk here) gives the same Gram to rounding."""
     import torch
     model = load_robot(robot)

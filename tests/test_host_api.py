@@ -225,3 +225,22 @@ def test_bench_traffic_source_is_the_newest_profile(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     traffic, src = bench.pmc_traffic("k2_gram_syrk", "spot", 20000)
     assert src.endswith(os.path.join("r03_p", "pmc_summary.json")) and traffic == 4
+
+
+def test_bench_traffic_source_mixed_tags(tmp_path, monkeypatch):
+    """A tag that starts with a digit (r03_2) sorts against a word tag (r03_j) without a type error: numbers
+    before words at the same position, so r03_j is the newer one."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for name, fetch in [("r03_2", 1.0), ("r03_j", 2.0), ("r02_10", 3.0)]:
+        d = tmp_path / "profiles" / name
+        d.mkdir(parents=True)
+        (d / "pmc_summary.json").write_text(json.dumps({
+            "_config": {"robot": "spot", "samples": 20000},
+            "k2_gram_syrk": {"FETCH_bytes_corrected_x2": fetch, "WRITE_bytes": 0.0}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    traffic, src = bench.pmc_traffic("k2_gram_syrk", "spot", 20000)
+    assert src.endswith(os.path.join("r03_j", "pmc_summary.json")) and traffic == 2
