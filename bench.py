@@ -178,7 +178,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from system_identification_amd.distributed import RcclGramComm, shard_range
+    from system_identification_amd.distributed import RcclGramComm, make_gram_exchange, shard_range
     from system_identification_amd.engine import EMIT_ALL, GRAM_PRECISION, GRAM_ROWS, Engine
     from system_identification_amd.model import load_robot
     from system_identification_amd.synthetic import channel_block, generate
@@ -206,27 +206,22 @@ def main():
     comm, exchange_name = None, None
     if world == 1 and args.exchange_world1:
         comm = RcclGramComm(eng, 0, 1)
-        exchange_name = "sysid_allreduce_gram (RCCL, C ABI, one-rank communicator: test mode)"
+        exchange_name = "sysid_allreduce_normal_equations (RCCL, C ABI, one-rank communicator: test mode)"
     if world > 1:
-        # the engine's own exchange step (C ABI: sysid_rccl_unique_id / _comm_init / sysid_allreduce_gram); the
-        # 128-byte RCCL id travels from rank 0 over the torch process group.  Should the C-ABI communicator fail
-        # to come up on some node, the same all-reduce runs through torch.distributed (RCCL) and the JSON says so.
+        # the engine's own exchange step (C ABI: sysid_rccl_unique_id / _comm_init /
+        # sysid_allreduce_normal_equations); the 128-byte RCCL id travels from rank 0 over the torch process group.
+        # Should the C-ABI communicator fail to come up on some rank, every rank runs the same all-reduce through
+        # torch.distributed (RCCL) and the JSON says so (distributed.make_gram_exchange).
         def share_id(raw):
             box = [raw if rank == 0 else None]
             dist.broadcast_object_list(box, src=0)
             return box[0]
-        try:
-            comm = RcclGramComm(eng, rank, world, share_id=share_id)
-            ok = torch.tensor([1], dtype=torch.int32, device="cuda")
-        except Exception as exc:  # noqa: BLE001 - reported in the JSON line
-            comm, exchange_name = None, f"torch.distributed.all_reduce (C-ABI RCCL init failed: {exc})"
-            ok = torch.tensor([0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same path
-        if int(ok.item()) == 0 and comm is not None:
-            comm.close()
-            comm, exchange_name = None, "torch.distributed.all_reduce (C-ABI RCCL init failed on another rank)"
-        if comm is not None:
-            exchange_name = "sysid_allreduce_gram (RCCL, C ABI)"
+
+        def all_ok(flag):
+            t = torch.tensor([int(flag)], dtype=torch.int32, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return int(t.item()) == 1
+        comm, exchange_name = make_gram_exchange(eng, rank, world, share_id, all_ok)
 
     if args.gram_only:
         # config 5: 16 GiB chunk panels (the library default is 4 GiB; 16 GiB measured 2-3% faster on G1 1M)
@@ -241,9 +236,12 @@ def main():
         def launch(s, b=bufs):
             eng.build_device(d_in, N, flags, b, stream=s)
 
+    xbuf = comm.exchange_buffer() if comm is not None else None
+    rows_local = float(N * model.nv)
+
     def exchange():
         if comm is not None:
-            comm.allreduce_gram(bufs["gram"], stream=stream.cuda_stream)
+            comm.allreduce_normal_equations(bufs["gram"], rows_local, xbuf, stream=stream.cuda_stream)
         elif world > 1:
             dist.all_reduce(bufs["gram"])
 
@@ -255,6 +253,7 @@ def main():
     bufsets = [bufs]
     if overlap:
         bufsets.append(dict(bufs, gram=torch.zeros_like(bufs["gram"])))
+        xbufs = [xbuf, comm.exchange_buffer()]
         comm_stream = torch.cuda.Stream(device=local)
         k_done = [torch.cuda.Event(), torch.cuda.Event()]
         x_done = [torch.cuda.Event(), torch.cuda.Event()]
@@ -288,7 +287,7 @@ def main():
             launch(stream.cuda_stream, bufsets[b])
             k_done[b].record(stream)
             comm_stream.wait_event(k_done[b])
-            comm.allreduce_gram(bufsets[b]["gram"], stream=comm_stream.cuda_stream)
+            comm.allreduce_normal_equations(bufsets[b]["gram"], rows_local, xbufs[b], stream=comm_stream.cuda_stream)
             x_done[b].record(comm_stream)
             x_used[b] = True
         else:
@@ -370,6 +369,9 @@ def main():
             torch.cuda.synchronize()
             exchange_check = {"bitwise_equal_local_build": all(bool(torch.equal(b_["gram"], ref_g["gram"]))
                                                                for b_ in bufsets), "buffers": len(bufsets)}
+        # the packed exchange carries the row count: the job's N·nv (the Solver's 1/num_rows, solver.py:190)
+        exchange_check["num_rows"] = float(xbuf[-1].item())
+        exchange_check["num_rows_ok"] = exchange_check["num_rows"] == float(total_per_step * model.nv)
 
     # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only: the chunked
     # path itself, each stage summed over its chunks.

@@ -87,7 +87,7 @@ extern "C" {
 typedef struct sysid_engine sysid_engine;
 
 /* ABI version (bumped on any signature or layout change). */
-int32_t sysid_abi_version(void);  /* 5 */
+int32_t sysid_abi_version(void);  /* 6 */
 
 /* Create an engine for one device from a packed model.  Replaces the model construction of
  * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
@@ -189,6 +189,14 @@ int32_t sysid_rccl_comm_init(void** comm, int32_t nranks, const void* id128, int
 int32_t sysid_rccl_comm_destroy(void* comm);
 int32_t sysid_allreduce_gram(const sysid_engine* e, double* d_gram, void* comm, void* stream);
 const char* sysid_rccl_last_error(void);
+/* The packed exchange: the upper triangle of the (W+1)x(W+1) device Gram (G, Aᵀb and bᵀb,
+ * row by row) plus the rank's row count, (W+1)(W+2)/2 + 1 doubles (Spot 12,091, G1 64,981 — half the
+ * bytes of sysid_allreduce_gram), summed by one RCCL all-reduce and unpacked into both triangles of d_gram
+ * (bitwise symmetric).  d_xbuf: a device buffer of sysid_exchange_bytes(e) bytes, 8-byte aligned; after the
+ * call its last element holds the summed row count (num_rows of the whole job).  Stream-ordered. */
+size_t sysid_exchange_bytes(const sysid_engine* e);
+int32_t sysid_allreduce_normal_equations(const sysid_engine* e, double* d_gram, double* d_xbuf, double rows,
+                                         void* comm, void* stream);
 
 /* Ingest: native reader of the reference's .dat logs (read_data,
  * demo/spot_identification.py:9-14): tab-delimited text, one channel per line, parsed like
@@ -222,6 +230,15 @@ int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12);
 int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4);
 /* K2 Gram deal chosen at model creation: {tile columns, tile slots of the f64, f32 and bf16 deals}. */
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
+
+/* Fused K1 + Gram (k12_fused_panel_gram): the full-output f64 path of the quadruped models (nv = 18, a 10-tile
+ * Gram: Spot, Solo-12) builds the stacked panel and the Gram in one launch, the Gram waves reading the panel back
+ * from L2 while the K1 waves of their workgroup produce it.  Same outputs and contract as
+ * sysid_build_device (the Gram differs from the unfused path's only in summation order, ~1e-16 relative).  On by
+ * default where supported (environment SYSID_FUSE=0 turns it off at engine creation); sysid_set_fusion switches
+ * it per engine; sysid_fused tells whether `flags` (with SYSID_EMIT_GRAM, f64, the engine's panel_ld) run fused. */
+int32_t sysid_set_fusion(sysid_engine* e, int32_t on);
+int32_t sysid_fused(const sysid_engine* e, uint32_t flags);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */
 int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6);
 

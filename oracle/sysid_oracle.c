@@ -347,17 +347,22 @@ int oracle_build(void* h, const double* q, const double* dq, const double* ddq, 
         if (Bv) memcpy(Bv + row * na, ar + wy, sizeof(double) * na);
         if (Bc) memcpy(Bc + row * na, ar + wy + na, sizeof(double) * na);
         if (tp) tp[row] = ar[W];
-        if (Gl) {
-          for (int a = 0; a < W; ++a) {
-            const double x = ar[a];
-            if (x == 0.0) continue;
-            double* Gr = Gl + (size_t)a * W;
-            for (int b = a; b < W; ++b) Gr[b] += x * ar[b];
-          }
-        }
         if (gl)
           for (int a = 0; a < W; ++a) gl[a] += ar[a] * ar[W];
         bbl += ar[W] * ar[W];
+      }
+      /* the sample's nv rows into the upper triangle, Gram row by Gram row (each Gram row read once per sample,
+       * not once per panel row: the thread's W x W partial stays in its cache) */
+      if (Gl) {
+        for (int a = 0; a < W; ++a) {
+          double* Gr = Gl + (size_t)a * W;
+          for (int r = 0; r < nv; ++r) {
+            const double* ar = A + r * (W + 1);
+            const double x = ar[a];
+            if (x == 0.0) continue;
+            for (int b = a; b < W; ++b) Gr[b] += x * ar[b];
+          }
+        }
       }
     }
 #pragma omp critical

@@ -67,6 +67,11 @@ struct sysid_engine {
     int blk = 0;  // the register-blocked kernel (k2_gram_syrk_blk / _bf16_blk): one workgroup per CU
     int2* d_tiles = nullptr;  // [super slots | tile slots]
   } k2d[3];
+  // K12: the fused K1 + Gram kernel of the full-output f64 path (quadruped K1, 10 tile columns): usable (k12_ok),
+  // enabled (fuse: sysid_set_fusion), its dynamic LDS and the K3 tile table of its slab slots
+  int k12_ok = 0, fuse = 1;
+  size_t k12_lds = 0;
+  int2* d_k12_tiles = nullptr;
   // host-API buffers (grow-only)
   double* d_in = nullptr;
   size_t in_cap = 0;
@@ -242,11 +247,50 @@ int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipSt
   return SYSID_OK;
 }
 
-// Workspace of sysid_build_device: [K1 counter | K2 slabs] (the slabs with EMIT_GRAM).
+// K12 (fused K1 + Gram): one workgroup per CU, at most one per sample pair.
+int64_t k12_grid(const sysid_engine* e, int64_t N) {
+  return std::max<int64_t>(1, std::min<int64_t>(e->cus, (N + 1) / 2));
+}
+size_t k12_slab_bytes(const sysid_engine* e, int64_t N) {
+  return align256((size_t)k12_grid(e, N) * K12_NSLOTS * 256 * sizeof(double));
+}
+// The full-output Gram runs fused when the model has the kernel, fusion is on, the Gram is f64 and the panel has
+// the engine's own leading dimension (the Gram waves read exactly the columns K1 writes).
+bool k12_active(const sysid_engine* e, uint32_t flags, int64_t ld_panel) {
+  return e->k12_ok && e->fuse && (flags & SYSID_EMIT_GRAM) && gram_prec(flags) == 0 && ld_panel == e->ldp;
+}
+
+int launch_k12(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
+               double* slab, hipStream_t st) {
+  K1Params kp = e->kp;
+  const sysid_engine::K1Shape& K = e->k1m[0];
+  kp.pov = 0;
+  kp.wave_dbl = K.wave_dbl;
+  kp.rg = k1_row_groups(kp.NJ, 64 / k1_spw(K.variant));
+  kp.out_cols = (int)std::min<int64_t>(ld_panel, e->ldp);
+  sysid_launch::k12_launch(dim3((unsigned)k12_grid(e, N)), e->k12_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel, ld_panel,
+                           slab);
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
+}
+
+int launch_k3_tiles(sysid_engine* e, int ks, const double* slab, const int2* tiles, int nslots, double* d_gram,
+                    hipStream_t st) {
+  const int64_t nx = (int64_t)nslots * 256;
+  hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, tiles, nx, ks, e->ncol,
+                     d_gram);
+  HIP_TRY(e, hipGetLastError());
+  return SYSID_OK;
+}
+
+// Workspace of sysid_build_device: [K1 counter | K2 slabs] (the slabs with EMIT_GRAM: room for the unfused K2's
+// and the fused kernel's, whichever runs).
 size_t stages_ws_bytes(const sysid_engine* e, int64_t N, uint32_t flags) {
   if (N <= 0) return 0;
   const int64_t rows = N * e->nv;
-  return WORK_BYTES + ((flags & SYSID_EMIT_GRAM) ? slab_bytes(e, rows) : 0);
+  size_t slabs = 0;
+  if (flags & SYSID_EMIT_GRAM) slabs = std::max(slab_bytes(e, rows), e->k12_ok ? k12_slab_bytes(e, N) : (size_t)0);
+  return WORK_BYTES + slabs;
 }
 
 // Every check of a launch sequence happens before its first enqueue: an error return means nothing was
@@ -273,6 +317,20 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   if (rc != SYSID_OK) return rc;
   const int64_t rows = N * e->nv;
   auto* work = static_cast<unsigned long long*>(d_ws);
+  if (k12_active(e, flags, ld_panel)) {
+    // fused: K1 + Gram in one launch (events: [0] -> [1] the fused kernel, [1] -> [2] empty, [2] -> [3] K3)
+    double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
+    if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
+    if ((rc = launch_k12(e, d_in, N, ld, d_panel, ld_panel, slab, st)) != SYSID_OK) return rc;
+    if (ev) {
+      HIP_TRY(e, hipEventRecord(ev[1], st));
+      HIP_TRY(e, hipEventRecord(ev[2], st));
+    }
+    if ((rc = launch_k3_tiles(e, (int)k12_grid(e, N), slab, e->d_k12_tiles, K12_NSLOTS, d_gram, st)) != SYSID_OK)
+      return rc;
+    if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
+    return SYSID_OK;
+  }
   if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
   if ((rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, work, st, nullptr)) != SYSID_OK) return rc;
   if (ev) HIP_TRY(e, hipEventRecord(ev[1], st));
@@ -455,7 +513,7 @@ int launch_k5(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_p
 
 extern "C" {
 
-int32_t sysid_abi_version(void) { return 5; }
+int32_t sysid_abi_version(void) { return 6; }
 
 const char* sysid_last_error(const sysid_engine* e) { return e ? e->err.c_str() : g_thread_error.c_str(); }
 
@@ -804,6 +862,27 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       sysid_destroy(e);
       return SYSID_E_MODEL;
     }
+    // the fused K1 + Gram kernel: the quadruped K1 beside the 10-column Gram waves, one workgroup per CU
+    if (e->k1m[0].variant == K1_C4_NV18 && e->ntc == K12_NTC) {
+      const size_t lds = (size_t)(MI.ndbl + K1_WAVES * k1_spw(K1_C4_NV18) * e->k1m[0].wave_dbl) * sizeof(double) +
+                         K1_WAVES * sizeof(int);
+      int nb = 0;
+      if (lds <= 160 * 1024 &&
+          hipFuncSetAttribute(sysid_launch::k12_fn(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sysid_launch::k12_fn(), 64 * (K1_WAVES + K12_GW), lds) ==
+              hipSuccess &&
+          nb >= 1) {
+        std::vector<int2> tl(K12_NSLOTS);
+        for (int k = 0; k < K12_NSLOTS; ++k) tl[k] = k12_tile(k);
+        st = hipMalloc(&e->d_k12_tiles, tl.size() * sizeof(int2));
+        if (st == hipSuccess) st = hipMemcpy(e->d_k12_tiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice);
+        e->k12_ok = st == hipSuccess ? 1 : 0;
+        e->k12_lds = lds;
+        if (const char* v = std::getenv("SYSID_FUSE")) e->fuse = std::atoi(v) != 0 ? 1 : 0;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
   }
   if (st != hipSuccess) {
     set_err(nullptr, SYSID_E_DEVICE, "device setup failed: %s", hipGetErrorString(st));
@@ -818,7 +897,7 @@ void sysid_destroy(sysid_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_in, (void*)e->d_panel,
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_k12_tiles, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1241,6 +1320,55 @@ int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4) {
   cfg4[2] = (int32_t)e->k1m[0].lds;
   cfg4[3] = e->k1_maxch_tpl;
   return SYSID_OK;
+}
+
+// The packed exchange's device side (sysid_rccl.cpp: sysid_allreduce_normal_equations): the upper triangle of the
+// n x n Gram row by row (row i starts at i n - i (i - 1) / 2), then the row count; unpacked into both triangles.
+__global__ void __launch_bounds__(256) xchg_pack(const double* __restrict__ G, int n, double rows,
+                                                 double* __restrict__ x) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n * n) return;
+  const int i = (int)(e / n), j = (int)(e - (int64_t)i * n);
+  if (j >= i) x[(int64_t)i * n - (int64_t)i * (i - 1) / 2 + (j - i)] = G[e];
+  if (e == 0) x[(int64_t)n * (n + 1) / 2] = rows;
+}
+__global__ void __launch_bounds__(256) xchg_unpack(const double* __restrict__ x, int n, double* __restrict__ G) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n * n) return;
+  const int r = (int)(e / n), c = (int)(e - (int64_t)r * n);
+  const int i = r < c ? r : c, j = r < c ? c : r;
+  G[e] = x[(int64_t)i * n - (int64_t)i * (i - 1) / 2 + (j - i)];
+}
+
+size_t sysid_exchange_bytes(const sysid_engine* e) {
+  if (!e) return 0;
+  const size_t n = (size_t)e->ncol;
+  return (n * (n + 1) / 2 + 1) * sizeof(double);
+}
+
+// sysid_rccl.cpp's hooks (one library, so the RCCL translation unit stays free of device code)
+int32_t sysid_internal_xchg_pack(const sysid_engine* e, const double* d_gram, double rows, double* d_x, void* stream) {
+  const int n = e->ncol;
+  hipLaunchKernelGGL(xchg_pack, dim3((unsigned)(((int64_t)n * n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_gram, n, rows, d_x);
+  return hipGetLastError() == hipSuccess ? SYSID_OK : SYSID_E_DEVICE;
+}
+int32_t sysid_internal_xchg_unpack(const sysid_engine* e, const double* d_x, double* d_gram, void* stream) {
+  const int n = e->ncol;
+  hipLaunchKernelGGL(xchg_unpack, dim3((unsigned)(((int64_t)n * n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_x, n, d_gram);
+  return hipGetLastError() == hipSuccess ? SYSID_OK : SYSID_E_DEVICE;
+}
+
+int32_t sysid_set_fusion(sysid_engine* e, int32_t on) {
+  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
+  e->fuse = on ? 1 : 0;
+  return SYSID_OK;
+}
+
+int32_t sysid_fused(const sysid_engine* e, uint32_t flags) {
+  if (!e) return SYSID_E_INVALID;
+  return k12_active(e, flags | SYSID_EMIT_GRAM, e->ldp) ? 1 : 0;
 }
 
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4) {

@@ -355,6 +355,9 @@ __device__ __forceinline__ double mgs_step_pair(const double* xp, double* x, dou
 // the Gram-only chunk panel of a reduced-precision Gram, f32 / bf16 — rounded once
 // here, so the Gram kernel stages 2x / 4x fewer bytes than from an f64 panel.
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef double dbl4 __attribute__((ext_vector_type(4)));  // MFMA accumulators and fragments
+typedef float flt4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ void panel_store(double* p, double a, double b) {
   *reinterpret_cast<double2*>(p) = make_double2(a, b);
 }
@@ -485,23 +488,26 @@ constexpr int K1_CMP_KMAX = 12;
 // formed; the column phases use G_i[r] = [r in S_i] J_r - Σ_j Q_j[r] K_ij with K_ij = Σ_{d in S_i} Q_j[d] J_d
 // (S_i: the free-flyer and chain dofs of body i), k reads per row instead of a chain of P entries and axes.
 constexpr int K1_QF_KMAX = 6;
-template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0>
-// Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
-// The P overlay's instantiations run 8 one-sample waves per workgroup (one 8-wave workgroup per CU).
-__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 || QF ? 2 : 1)
-k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
-                   int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
-                   unsigned long long* __restrict__ work, double* __restrict__ dbg,
-                   int* __restrict__ rcount) {
+// K1's per-wave body, shared by the standalone K1 (k1_regressor_panel, FUSED = 0: samples claimed from device
+// counters) and the K1 waves of the fused kernel (k12_fused_panel_gram, FUSED = 1: the workgroup's sample range
+// [f0, f1) dealt statically, wave w taking steps w, w + K1_WAVES, ...; after each step's panel stores have
+// completed the wave publishes its step count in k12_ready[w] (LDS) for the Gram waves of its workgroup).
+template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0, int FUSED = 0>
+__device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __restrict__ mimg_g,
+                                        const double* __restrict__ in, int64_t N, int64_t ld,
+                                        OutT* __restrict__ panel, int64_t ldp, unsigned long long* __restrict__ work,
+                                        double* __restrict__ dbg, int* __restrict__ rcount, int* k12_ready,
+                                        int64_t f0, int64_t f1) {
   static_assert(!(POV && CMP), "the nullspace mode runs the plain layout");
   static_assert(!QF || (NVC == 0 && !POV && !CMP), "the Q-form is a runtime-nv, plain-layout kernel");
+  static_assert(!FUSED || (!CMP && !POV && !QF), "the fused kernel runs the plain projector-row layout");
   extern __shared__ double smem[];
   const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
-  {
+  if constexpr (!FUSED) {
     uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
     for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
+    __syncthreads();  // the only workgroup barrier: the model image is read-only from here on
   }
-  __syncthreads();  // the only workgroup barrier: the model image is read-only from here on
 
   const int* mi = reinterpret_cast<const int*>(smem);
   const int* parent = mi + MI.parent;
@@ -560,8 +566,10 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   const int home = (int)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (K1_SHARDS - 1));  // XCC_ID
   auto shard_begin = [&](int x) -> int64_t { return x >= K1_SHARDS ? N : (N * x / K1_SHARDS) / SPW * SPW; };
   int sh = 0;  // shards (counted from home) found exhausted by this wave
+  int64_t fnext = f0 + (int64_t)SPW * wave;  // FUSED: the wave's next step in the static deal
   auto claim_issue = [&]() -> unsigned long long {
     unsigned long long v = 0;
+    if constexpr (FUSED) return v;
     if (lane == 0) {
       // an opaque (per-lane) offset keeps the atomic optimizer from rewriting the claim as a wave scan,
       // which reads the returned value (and waits for it) right at the atomic
@@ -579,6 +587,11 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   // the sample of a claim issued on the current shard, or (that shard exhausted) the next claim that succeeds
   // on the following shards, or N when every shard is exhausted
   auto claim_value = [&](unsigned long long raw) -> int64_t {
+    if constexpr (FUSED) {
+      const int64_t v = fnext;
+      fnext += (int64_t)SPW * K1_WAVES;
+      return v < f1 ? v : N;
+    }
     unsigned long long v = uniform64(raw);
     bool have = true;  // v is a claim on shard (home + sh)
     while (sh < K1_SHARDS) {
@@ -628,6 +641,13 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
   // issues first when its operands arrive (K1 -1 to -2%, Spot and G1)
   __builtin_amdgcn_s_setprio(2);
   const int hl_outer = hl;
+  int steps_done = 0;  // FUSED: steps whose panel stores have completed are published
+  auto publish = [&](int n) {
+    if constexpr (FUSED) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's panel stores have reached L2
+      if (lane == 0) __hip_atomic_store(k12_ready + wave, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
   while (s < N) {
     // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
     // step, so the per-lane index arithmetic of the phase loops (nv is a compile-time constant) and the
@@ -1277,6 +1297,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     wsync();
     if (s1 < N) commit();
     wsync();
+    // the previous step's stores were issued before this step's input prefetch, which commit() has just waited
+    // for: publishing them here costs no extra wait
+    if (steps_done > 0) publish(steps_done);
 
     __builtin_amdgcn_s_setprio(0);
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
@@ -1688,6 +1711,178 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
     __builtin_amdgcn_s_setprio(2);
     s = s1;
     s1 = s2;
+    ++steps_done;
+  }
+  publish(steps_done);
+}
+
+template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0>
+// Two-sample waves are held to 256 registers (2 waves per SIMD, which the LDS budget allows there).
+// The P overlay's instantiations run 8 one-sample waves per workgroup (one 8-wave workgroup per CU).
+__global__ void __launch_bounds__(POV ? 512 : 64 * K1_WAVES, SPW == 2 || QF ? 2 : 1)
+k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
+                   int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
+                   unsigned long long* __restrict__ work, double* __restrict__ dbg,
+                   int* __restrict__ rcount) {
+  k1_body<MAXCH, NVC, SPW, OutT, POV, CMP, QF, 0>(kp, mimg_g, in, N, ld, panel, ldp, work, dbg, rcount, nullptr, 0,
+                                                  0);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K12: K1 and the Gram in one launch (narrow Grams of 10 tile columns fed by the quadruped K1: Spot, Solo-12).
+//
+// K1 is VALU / LDS bound at two waves per SIMD and K2 is MFMA bound; run one after the other they use one pipe
+// at a time.  Here every workgroup (one per CU) holds 4 K1 waves and 4 Gram waves, one of each per SIMD, and the
+// SIMD's VALU and matrix pipes run side by side (MI355X_MICROARCH.md, "MFMA and VALU pipes are separate").
+// The samples are dealt statically: workgroup b takes the sample pairs [P b / G, P (b+1) / G), its K1 wave w the
+// pairs w, w + 4, ... of that range (k1_body, FUSED = 1), writing the stacked panel to HBM as the standalone K1
+// does.  A K1 wave publishes, in LDS, how many of its steps have completed (their stores acknowledged by L2:
+// s_waitcnt vmcnt(0)); the Gram waves walk the workgroup's pairs in order and read each pair's 36 rows back from
+// L2 as MFMA fragments (nontemporal loads, served by L2, never by a possibly stale L1 line), accumulating their
+// tiles in registers: no LDS staging, no barrier, and no re-read of the panel from HBM.  Each Gram wave owns a
+// fixed set of the Gram's 55 upper 16x16 tiles (k12_role: block columns paired high with low, 14/14/14/13
+// tiles) and writes them to its workgroup's slab once at the end; K3 sums the slabs as after K2.
+// Deterministic: the deal, the pair order and every accumulation order are fixed.
+// No Gram wave waits on anything but its own workgroup's K1 waves, which never wait on it, so the launch cannot
+// deadlock; a wait still gives up after ~1 s and poisons its tiles with NaN (a bug must not hang the GPU).
+// ------------------------------------------------------------------------------------------------
+constexpr int K12_NTC = 10;
+constexpr int K12_GW = 4;        // Gram waves per workgroup (waves 4..7: one per SIMD)
+constexpr int K12_NSLOTS = 55;   // upper tiles of a 10 x 10 tile Gram
+struct K12Role {
+  int nc;        // tile columns of the role
+  int col[4];    // their block column J
+  int nrow[4];   // tiles (I = 0 .. nrow - 1) of each
+  int base;      // first slab slot
+  int ntiles;
+};
+__host__ __device__ constexpr K12Role k12_role(int w) {
+  return w == 0 ? K12Role{2, {9, 3, 0, 0}, {10, 4, 0, 0}, 0, 14}
+       : w == 1 ? K12Role{2, {8, 4, 0, 0}, {9, 5, 0, 0}, 14, 14}
+       : w == 2 ? K12Role{2, {7, 5, 0, 0}, {8, 6, 0, 0}, 28, 14}
+                : K12Role{4, {6, 2, 1, 0}, {7, 3, 2, 1}, 42, 13};
+}
+// slab slot -> (I, J) block coordinates (host: the K3 tile table; device: the fragments of a tile)
+__host__ __device__ constexpr int2 k12_tile(int slot) {
+  int w = 3;
+  while (w > 0 && k12_role(w).base > slot) --w;
+  const K12Role R = k12_role(w);
+  int t = slot - R.base;
+  for (int c = 0; c < R.nc; ++c) {
+    if (t < R.nrow[c]) return int2{t, R.col[c]};
+    t -= R.nrow[c];
+  }
+  return int2{-1, -1};
+}
+
+template <int W, int NVC>
+__device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, int64_t ldp, int64_t f0, int64_t f1,
+                                              const int* k12_ready, double* __restrict__ slab) {
+  constexpr K12Role R = k12_role(W);
+  constexpr int NB = R.col[0] + 1;         // fragment blocks 0 .. col[0] (every role's first column is its widest)
+  constexpr int NT = R.ntiles;
+  constexpr int KSP = (2 * NVC + 3) / 4;   // k-steps (4 rows) per pair of samples
+  const int lane = threadIdx.x & 63, kr = lane >> 4, kc = lane & 15;
+  const int64_t np = (f1 - f0 + 1) / 2;
+  const int64_t U = np * KSP;              // units = (pair, k-step)
+  dbl4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  bool bad = false;
+  // a pair is ready once its K1 wave (pair % 4) has published step pair / 4
+  auto wait_pair = [&](int64_t p) {
+    const int v = (int)(p & (K1_WAVES - 1)), need = (int)(p / K1_WAVES) + 1;
+    int spins = 0;
+    while (__hip_atomic_load(k12_ready + v, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 23)) {  // ~1 s: never expected; give up rather than hang the device
+        bad = true;
+        break;
+      }
+    }
+  };
+  // the issue cursor (pair ip, k-step ik) of the next unit to load; loads past the last unit repeat it
+  int64_t ip = 0;
+  int ik = 0;
+  auto issue = [&](double (&f)[NB]) {
+    if (ik == 0 && ip < np && !bad) wait_pair(ip);
+    const int64_t p = ip < np ? ip : np - 1;
+    const int k = ip < np ? ik : KSP - 1;
+    const int64_t s0 = f0 + 2 * p;
+    const int nrows = (f1 - s0 >= 2 ? 2 : 1) * NVC;
+    const int r = 4 * k + kr;
+    const bool rok = r < nrows;
+    const double* rowp = panel + (s0 * NVC + (rok ? r : 0)) * ldp + kc;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const bool ok = rok && (16 * b + kc < ldp);
+      const double x = __builtin_nontemporal_load(rowp + (ok ? 16 * b : 0));
+      f[b] = ok ? x : 0.0;
+    }
+    if (++ik == KSP) {
+      ik = 0;
+      ++ip;
+    }
+  };
+  auto mma = [&](const double (&f)[NB]) {
+    int t = 0;
+#pragma unroll
+    for (int c = 0; c < R.nc; ++c)
+#pragma unroll
+      for (int i = 0; i < R.nrow[c]; ++i) {
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[i], f[R.col[c]], acc[t], 0, 0, 0);
+        ++t;
+      }
+  };
+  // three units in flight: unit u + 2 is requested while unit u is multiplied
+  double fa[NB], fb[NB], fc[NB];
+  if (U > 0) {
+    issue(fa);
+    issue(fb);
+  }
+  static_assert(KSP % 3 == 0, "whole rounds of three units per pair");
+  for (int64_t u = 0; u < U; u += 3) {
+    issue(fc);
+    mma(fa);
+    issue(fa);
+    mma(fb);
+    issue(fb);
+    mma(fc);
+  }
+  double* o = slab + ((size_t)blockIdx.x * K12_NSLOTS + R.base) * 256;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[t * 256 + (kr + 4 * j) * 16 + kc] = bad ? __builtin_nan("") : acc[t][j];
+}
+
+template <int MAXCH, int NVC, int SPW>
+__global__ void __launch_bounds__(64 * (K1_WAVES + K12_GW), 2)
+k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
+                     int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp, double* __restrict__ slab) {
+  static_assert(NVC == 18 && SPW == 2, "the fused kernel serves the quadruped K1 (two samples per wave)");
+  extern __shared__ double smem[];
+  int* ready = reinterpret_cast<int*>(smem + kp.mimg_dbl + K1_WAVES * SPW * kp.wave_dbl);
+  {
+    uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
+    for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
+    if (threadIdx.x < K1_WAVES) ready[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const int64_t P = (N + SPW - 1) / SPW;
+  const int64_t p0 = P * blockIdx.x / gridDim.x, p1 = P * (blockIdx.x + 1) / gridDim.x;
+  const int64_t f0 = p0 * SPW, f1 = p1 * SPW < N ? p1 * SPW : N;
+  const int wave = threadIdx.x >> 6;
+  if (wave < K1_WAVES) {
+    k1_body<MAXCH, NVC, SPW, double, 0, 0, 0, 1>(kp, mimg_g, in, N, ld, panel, ldp, nullptr, nullptr, nullptr, ready,
+                                                 f0, f1);
+  } else {
+    switch (wave - K1_WAVES) {
+      case 0: k12_gram_wave<0, NVC>(panel, ldp, f0, f1, ready, slab); break;
+      case 1: k12_gram_wave<1, NVC>(panel, ldp, f0, f1, ready, slab); break;
+      case 2: k12_gram_wave<2, NVC>(panel, ldp, f0, f1, ready, slab); break;
+      default: k12_gram_wave<3, NVC>(panel, ldp, f0, f1, ready, slab); break;
+    }
   }
 }
 
@@ -1772,9 +1967,6 @@ k1s_row_list(const int* __restrict__ rcount, const int* __restrict__ rseg, int n
 // Fragment = 16 consecutive doubles of 4 consecutive rows: lane l holds row (l>>4), col (l&15), which is
 // both the A layout (A[i=l&15][k=l>>4]) and the B layout (B[k=l>>4][j=l&15]) of v_mfma_f64_16x16x4_f64.
 // ------------------------------------------------------------------------------------------------
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-typedef float flt4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Waves per K2 workgroup and super-tile slots per wave, by Gram width: narrow Grams (one workgroup holds every
 // super-tile, Spot: 16 pieces) run 16 waves of one slot each -- four waves per SIMD hide the per-chunk barrier
 // and fragment-read latency better than two waves of two slots (Spot K2 -3.9%, profiles/r02_ab2/k2_waves16_ab.txt);

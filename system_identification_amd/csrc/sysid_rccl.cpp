@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdint>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -115,6 +116,29 @@ int32_t sysid_allreduce_gram(const sysid_engine* e, double* d_gram, void* comm, 
   const ncclResult_t st = r->all_reduce(d_gram, d_gram, (size_t)cols * (size_t)cols, ncclFloat64, ncclSum,
                                         static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(stream));
   return st == ncclSuccess ? SYSID_OK : fail(st, r, "ncclAllReduce");
+}
+
+int32_t sysid_internal_xchg_pack(const sysid_engine* e, const double* d_gram, double rows, double* d_x, void* stream);
+int32_t sysid_internal_xchg_unpack(const sysid_engine* e, const double* d_x, double* d_gram, void* stream);
+
+int32_t sysid_allreduce_normal_equations(const sysid_engine* e, double* d_gram, double* d_xbuf, double rows,
+                                         void* comm, void* stream) {
+  if (!e || !d_gram || !d_xbuf || !comm || (reinterpret_cast<uintptr_t>(d_xbuf) & 7)) return SYSID_E_INVALID;
+  Rccl* r = rccl();
+  if (!r) return SYSID_E_DEVICE;
+  const size_t count = sysid_exchange_bytes(e) / sizeof(double);
+  if (sysid_internal_xchg_pack(e, d_gram, rows, d_xbuf, stream) != SYSID_OK) {
+    g_rccl_error = "pack kernel launch failed";
+    return SYSID_E_DEVICE;
+  }
+  const ncclResult_t st = r->all_reduce(d_xbuf, d_xbuf, count, ncclFloat64, ncclSum, static_cast<ncclComm_t>(comm),
+                                        static_cast<hipStream_t>(stream));
+  if (st != ncclSuccess) return fail(st, r, "ncclAllReduce");
+  if (sysid_internal_xchg_unpack(e, d_xbuf, d_gram, stream) != SYSID_OK) {
+    g_rccl_error = "unpack kernel launch failed";
+    return SYSID_E_DEVICE;
+  }
+  return SYSID_OK;
 }
 
 }  // extern "C"

@@ -47,20 +47,38 @@ def unpack_normal_equations(buf, num_rows: int) -> dict:
     return {"gram": buf[:W, :W].copy(), "Atb": buf[:W, W].copy(), "btb": float(buf[W, W]), "num_rows": int(num_rows)}
 
 
+def pack_upper(buf, rows) -> np.ndarray:
+    """The exchange format of SURVEY.md §8e (and of the device's sysid_allreduce_normal_equations): the upper
+    triangle of the n x n buffer row by row (row i at i n - i (i - 1) / 2), then the row count: n (n + 1) / 2 + 1
+    doubles (Spot 12,091, G1 64,981)."""
+    buf = np.asarray(buf, dtype=np.float64)
+    n = buf.shape[0]
+    return np.concatenate([buf[np.triu_indices(n)], [float(rows)]])
+
+
+def unpack_upper(x, n: int):
+    """Inverse of pack_upper: the symmetric n x n buffer (both triangles from the packed one) and the row count."""
+    x = np.asarray(x, dtype=np.float64)
+    buf = np.empty((n, n))
+    iu = np.triu_indices(n)
+    buf[iu] = x[:-1]
+    buf.T[iu] = x[:-1]
+    return buf, x[-1]
+
+
 def allreduce_normal_equations(ne: dict, device=None, group=None) -> dict:
-    """Sum the per-rank normal equations over the process group (one collective of the packed buffer
-    plus the row count riding in the same buffer's spare element)."""
+    """Sum the per-rank normal equations over the process group: one collective of the packed upper triangle
+    of [[G, g], [gᵀ, bᵀb]] plus the row count (pack_upper)."""
     import torch
     import torch.distributed as dist
     buf, rows = pack_normal_equations(ne)
-    W1 = buf.shape[0]
-    flat = np.concatenate([buf.reshape(-1), [float(rows)]])
-    t = torch.from_numpy(flat)
+    n = buf.shape[0]
+    t = torch.from_numpy(pack_upper(buf, rows))
     if device is not None:
         t = t.to(device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    out = t.cpu().numpy()
-    return unpack_normal_equations(out[:-1].reshape(W1, W1), int(round(out[-1])))
+    out, total = unpack_upper(t.cpu().numpy(), n)
+    return unpack_normal_equations(out, int(round(total)))
 
 
 def build_normal_equations_distributed(q, dq, ddq, tau, cnt, build_partial: Callable, rank: int, world: int,
@@ -110,6 +128,24 @@ class RcclGramComm:
                                          ctypes.c_void_p(st)) != 0:
             raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
 
+    def exchange_buffer(self):
+        """A device buffer for allreduce_normal_equations (sysid_exchange_bytes)."""
+        import torch
+        n = int(self.lib.sysid_exchange_bytes(self.engine._h)) // 8
+        return torch.zeros(n, dtype=torch.float64, device=torch.device("cuda", self.engine.device))
+
+    def allreduce_normal_equations(self, gram, rows: float, xbuf, stream=None):
+        """The packed exchange: the upper triangle of the (W+1)x(W+1) Gram plus this rank's row
+        count, (W+1)(W+2)/2 + 1 doubles in one all-reduce; the Gram is rewritten with the sums (both triangles) and
+        xbuf[-1] holds the job's row count.  Stream-ordered."""
+        import ctypes
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream(self.engine.device).cuda_stream
+        if self.lib.sysid_allreduce_normal_equations(self.engine._h, ctypes.c_void_p(gram.data_ptr()),
+                                                      ctypes.c_void_p(xbuf.data_ptr()), float(rows), self._comm,
+                                                      ctypes.c_void_p(st)) != 0:
+            raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
+
     def close(self):
         if getattr(self, "_comm", None) and self._comm.value:
             self.lib.sysid_rccl_comm_destroy(self._comm)
@@ -120,3 +156,24 @@ class RcclGramComm:
             self.close()
         except Exception:
             pass
+
+
+def make_gram_exchange(engine, rank: int, world: int, share_id: Callable, all_ok: Callable, comm_cls=None):
+    """The multi-GPU exchange step bench.py runs (and a non-Python host would): the engine's own C-ABI RCCL
+    communicator (RcclGramComm), or, when its set-up fails on ANY rank, no communicator, so that every rank falls
+    back to the same torch.distributed all-reduce.  ``share_id(raw) -> bytes`` hands rank 0's 128-byte id to
+    the others; ``all_ok(flag) -> bool`` is the minimum of a 0/1 flag over the ranks (a collective).  Returns
+    (comm or None, a name for the JSON line)."""
+    comm_cls = comm_cls or RcclGramComm
+    comm, name = None, None
+    try:
+        comm = comm_cls(engine, rank, world, share_id=share_id)
+        ok = 1
+    except Exception as exc:  # noqa: BLE001 - the reason is reported
+        comm, name, ok = None, f"torch.distributed.all_reduce (C-ABI RCCL init failed: {exc})", 0
+    if not all_ok(ok) and comm is not None:
+        comm.close()
+        comm, name = None, "torch.distributed.all_reduce (C-ABI RCCL init failed on another rank)"
+    if comm is not None:
+        name = "sysid_allreduce_normal_equations (RCCL, C ABI, packed upper triangle + row count)"
+    return comm, name

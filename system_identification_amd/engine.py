@@ -58,6 +58,8 @@ SIGNATURES = [
     ("sysid_gram_rows", _c.c_int32, [_vp, _c.c_uint32]),
     ("sysid_set_gram_chunk_bytes", _c.c_int32, [_vp, _c.c_uint64]),
     ("sysid_debug_k2_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
+    ("sysid_set_fusion", _c.c_int32, [_vp, _c.c_int32]),
+    ("sysid_fused", _c.c_int32, [_vp, _c.c_uint32]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
@@ -70,6 +72,8 @@ SIGNATURES = [
     ("sysid_rccl_comm_destroy", _c.c_int32, [_vp]),
     ("sysid_allreduce_gram", _c.c_int32, [_vp, _vp, _vp, _vp]),
     ("sysid_rccl_last_error", _c.c_char_p, []),
+    ("sysid_exchange_bytes", _c.c_size_t, [_vp]),
+    ("sysid_allreduce_normal_equations", _c.c_int32, [_vp, _vp, _vp, _c.c_double, _vp, _vp]),
     ("sysid_tau_error", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _dp, _dp]),
     ("sysid_tau_error_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
     ("sysid_tau_error_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _vp, _vp, _vp, _c.c_size_t, _vp]),
@@ -375,6 +379,14 @@ class Engine:
         """Chunk panel size of the Gram-only path (>= 1 MiB; 0 = the 4 GiB default).  alloc_gram_device /
         gram_workspace_bytes follow it, so set it before allocating."""
         self._check(self.lib.sysid_set_gram_chunk_bytes(self._h, int(nbytes)))
+
+    def set_fusion(self, on: bool) -> None:
+        """Fused K1 + Gram for the full-output f64 Gram (sysid_set_fusion; on by default where supported)."""
+        self._check(self.lib.sysid_set_fusion(self._h, 1 if on else 0))
+
+    def fused(self, flags: int = EMIT_ALL) -> bool:
+        """Whether build_device with these flags (and the engine's panel ld) runs the fused K1 + Gram kernel."""
+        return self.lib.sysid_fused(self._h, int(flags)) == 1
 
     def gram_rows(self, precision: str = "f64", rows: str = "auto") -> str:
         """The rows build_gram_device uses: "nullspace" (Zᵀ·A) or "projector" (P·A)."""

@@ -134,3 +134,104 @@ def test_row_count_survives_the_float_buffer():
             dist.destroy_process_group()
     assert out["num_rows"] == 2 ** 40 + 12345 and isinstance(out["num_rows"], int)
     assert np.array_equal(out["gram"], ne["gram"]) and np.array_equal(out["Atb"], ne["Atb"]) and out["btb"] == 2.5
+
+
+def test_packed_upper_triangle_layout():
+    """pack_upper is the device exchange format (xchg_pack: row i of the upper triangle at i n - i (i - 1) / 2,
+    the row count last): §8e's 12,091 doubles for Spot and 64,981 for G1, and a bitwise-symmetric unpack."""
+    from system_identification_amd.distributed import pack_upper, unpack_upper
+    for n, want in ((155, 12091), (360, 64981)):
+        rng = np.random.default_rng(n)
+        A = rng.normal(size=(n + 5, n))
+        G = A.T @ A
+        x = pack_upper(G, 17)
+        assert x.size == want
+        for i in (0, 1, n // 2, n - 1):
+            off = i * n - i * (i - 1) // 2
+            assert np.array_equal(x[off:off + n - i], G[i, i:])
+        back, rows = unpack_upper(x, n)
+        assert rows == 17 and np.array_equal(back, back.T) and np.array_equal(np.triu(back), np.triu(G))
+
+
+class _StubLib:
+    """The five RCCL entry points of libsysid.so as RcclGramComm calls them (ctypes-style arguments), with
+    scripted failures; records what it was given."""
+
+    def __init__(self, fail_id=False, fail_init=False):
+        self.fail_id, self.fail_init = fail_id, fail_init
+        self.init_ids, self.destroyed = [], 0
+
+    def sysid_rccl_unique_id(self, buf):
+        if self.fail_id:
+            return -3
+        buf.raw = bytes((7 * k + 3) % 256 for k in range(128))
+        return 0
+
+    def sysid_rccl_last_error(self):
+        return b"stub: scripted failure"
+
+    def sysid_rccl_comm_init(self, comm_ref, world, uid, rank, device):
+        self.init_ids.append(bytes(uid.raw))
+        if self.fail_init:
+            return -3
+        comm_ref._obj.value = 4096 + rank
+        return 0
+
+    def sysid_rccl_comm_destroy(self, comm):
+        self.destroyed += 1
+        return 0
+
+
+def _worker_exchange(rank, world, port, scenario, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import json
+    import torch
+    import torch.distributed as dist
+    from system_identification_amd.distributed import make_gram_exchange
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lib = _StubLib(fail_id=(scenario == "id_fails" and rank == 0), fail_init=(scenario == "init_fails" and rank == 1))
+
+    class Eng:
+        pass
+    eng = Eng()
+    eng.lib, eng.device, eng._h = lib, 0, None
+
+    def share_id(raw):
+        box = [raw if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def all_ok(flag):
+        t = torch.tensor([int(flag)], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item()) == 1
+    comm, name = make_gram_exchange(eng, rank, world, share_id, all_ok)
+    with open(out_path + f".{rank}.json", "w") as f:
+        json.dump({"comm": comm is not None, "name": name, "ids": [i.hex() for i in lib.init_ids],
+                   "destroyed": lib.destroyed}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scenario", ["ok", "init_fails", "id_fails"])
+def test_rccl_exchange_setup_world2(tmp_path, scenario):
+    """RcclGramComm's id sharing and bench.py's fallback (distributed.make_gram_exchange) on two gloo ranks with a
+    stub library: every rank initialises with rank 0's 128-byte id; if the C-ABI set-up fails on any rank, EVERY
+    rank falls back to torch.distributed (and a communicator that did come up is destroyed)."""
+    import json
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "x")
+    mp.start_processes(_worker_exchange, args=(2, _free_port(), scenario, out), nprocs=2, start_method="spawn")
+    r = [json.load(open(out + f".{k}.json")) for k in range(2)]
+    want_id = bytes((7 * k + 3) % 256 for k in range(128)).hex()
+    if scenario == "ok":
+        assert all(x["comm"] for x in r) and all(x["ids"] == [want_id] for x in r)
+        assert all("sysid_allreduce_normal_equations" in x["name"] for x in r)
+    elif scenario == "init_fails":
+        assert not any(x["comm"] for x in r)
+        assert r[0]["ids"] == [want_id] and r[1]["ids"] == [want_id]
+        assert r[0]["destroyed"] == 1 and "another rank" in r[0]["name"]
+        assert "init failed" in r[1]["name"]
+    else:  # rank 0 has no id: nobody calls comm_init, both fall back
+        assert not any(x["comm"] for x in r) and all(x["ids"] == [] for x in r)
+        assert all("init failed" in x["name"] for x in r)

@@ -1,0 +1,91 @@
+"""The fused K1 + Gram kernel (k12_fused_panel_gram) against the unfused K1 -> K2 -> K3 path and
+the C oracle: Spot and Solo-12 (the quadruped K1, 10-tile Gram), ragged sample counts (an odd last pair, fewer
+pairs than CUs, one sample), bitwise repeatability and graph replay.  Reference: demo/spot_identification.py:84-87
+(the stacked panel) and src/solver.py:186-190 (the Gram the objective implies)."""
+import numpy as np
+import pytest
+
+from oracle.ref_c import COracle
+from system_identification_amd.engine import EMIT_ALL, Engine
+from system_identification_amd.model import load_robot
+from system_identification_amd.synthetic import channel_block, generate
+
+pytestmark = pytest.mark.gpu
+
+CH = ("q", "dq", "ddq", "tau", "contact")
+
+
+def rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def run(e, d, N, fused):
+    import torch
+    e.set_fusion(fused)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_device(N, EMIT_ALL)
+    bufs["gram"].fill_(np.nan)
+    e.build_device(din, N, EMIT_ALL, bufs)
+    torch.cuda.synchronize()
+    return bufs["panel"][: N * e.nv].cpu().numpy(), bufs["gram"].cpu().numpy()
+
+
+def test_fused_where_supported():
+    for robot, want in (("spot", True), ("solo12", True), ("g1_29dof", False), ("snake14", False)):
+        e = Engine(load_robot(robot))
+        assert e.fused(EMIT_ALL) == want, robot
+        e.set_fusion(False)
+        assert not e.fused(EMIT_ALL)
+
+
+@pytest.mark.parametrize("robot,N", [("spot", 1), ("spot", 3), ("spot", 64), ("spot", 513), ("spot", 20000),
+                                     ("solo12", 2000), ("solo12", 4001)])
+def test_fused_matches_unfused_and_oracle(robot, N):
+    model = load_robot(robot)
+    e = Engine(model)
+    d = generate(model, N, config_index=5)
+    P1, G1 = run(e, d, N, True)
+    P0, G0 = run(e, d, N, False)
+    # the panel: the same K1 code on the same samples
+    assert rel(P1, P0) <= 1e-15, robot
+    # the Gram: another summation order only
+    W = e.panel_cols
+    assert np.all(np.isfinite(G1))
+    assert rel(G1, G0) <= 1e-13, (robot, N, rel(G1, G0))
+    assert np.array_equal(G1, G1.T)
+    # whole-N C oracle (OpenMP): Gram, Atb, btb at north_star's 1e-6
+    o = COracle(model).build(*[d[k] for k in CH], nthreads=16, stacked=False)
+    Wg = W - 1
+    assert rel(G1[:Wg, :Wg], o["gram"]) < 1e-6
+    assert rel(G1[:Wg, Wg], o["Atb"]) < 1e-6
+    assert abs(G1[Wg, Wg] - o["btb"]) <= 1e-6 * abs(o["btb"])
+
+
+def test_fused_bitwise_repeatable_and_graph_replay():
+    import torch
+    model = load_robot("spot")
+    e = Engine(model)
+    N = 20000
+    d = generate(model, N, config_index=6)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_device(N, EMIT_ALL)
+    e.build_device(din, N, EMIT_ALL, bufs)
+    torch.cuda.synchronize()
+    P, G = bufs["panel"].clone(), bufs["gram"].clone()
+    for _ in range(3):
+        bufs["gram"].zero_()
+        e.build_device(din, N, EMIT_ALL, bufs)
+        torch.cuda.synchronize()
+        assert torch.equal(bufs["gram"], G) and torch.equal(bufs["panel"], P)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        e.build_device(din, N, EMIT_ALL, bufs, stream=s.cuda_stream)  # warm outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        e.build_device(din, N, EMIT_ALL, bufs, stream=torch.cuda.current_stream().cuda_stream)
+    for _ in range(3):
+        bufs["gram"].zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(bufs["gram"], G) and torch.equal(bufs["panel"], P)
