@@ -10,6 +10,9 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and the built libsysid.so")
+    # the slowest tests' run times at the end of every run (the whole-N oracle parity tests report theirs)
+    if getattr(config.option, "durations", None) is None:
+        config.option.durations = 12
 
 
 REFERENCE = os.environ.get("SYSID_REFERENCE", "/root/reference")
