@@ -1776,15 +1776,15 @@ __host__ __device__ constexpr int2 k12_tile(int slot) {
 }
 
 template <int W, int NVC>
-__device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, int64_t ldp, int64_t f0, int64_t f1,
-                                              const int* k12_ready, double* __restrict__ slab) {
+__device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, int64_t ldp, int64_t N, int64_t f0,
+                                              int64_t f1, const int* k12_ready, double* __restrict__ slab) {
   constexpr K12Role R = k12_role(W);
   constexpr int NB = R.col[0] + 1;         // fragment blocks 0 .. col[0] (every role's first column is its widest)
   constexpr int NT = R.ntiles;
   constexpr int KSP = (2 * NVC + 3) / 4;   // k-steps (4 rows) per pair of samples
+  static_assert(KSP == 9, "the unit schedule below is written for 36-row pairs");
   const int lane = threadIdx.x & 63, kr = lane >> 4, kc = lane & 15;
   const int64_t np = (f1 - f0 + 1) / 2;
-  const int64_t U = np * KSP;              // units = (pair, k-step)
   dbl4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -1801,27 +1801,31 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
       }
     }
   };
-  // the issue cursor (pair ip, k-step ik) of the next unit to load; loads past the last unit repeat it
-  int64_t ip = 0;
-  int ik = 0;
-  auto issue = [&](double (&f)[NB]) {
-    if (ik == 0 && ip < np && !bad) wait_pair(ip);
-    const int64_t p = ip < np ? ip : np - 1;
-    const int k = ip < np ? ik : KSP - 1;
+  // Loads are unconditional (a masked load became an exec-masked branch with its own vmcnt(0) wait) at
+  // immediate offsets 16 b from one row address.  Lanes of block 9 whose column is past the row (16 b + kc >=
+  // ldp) read the next row's first columns: what they add lands only in Gram entries past column ldp - 1, which
+  // K3 never writes.  The panel's very last pair is the exception (those reads would run past the panel, and an
+  // odd last sample leaves half the pair's rows unwritten): its units clamp the column into the row and the row
+  // into the pair, and scale missing rows by 0 (the clamped address reads a finite panel value).
+  auto pair_base = [&](int64_t p, const double*& base, int& nrows) {
     const int64_t s0 = f0 + 2 * p;
-    const int nrows = (f1 - s0 >= 2 ? 2 : 1) * NVC;
+    nrows = (f1 - s0 >= 2 ? 2 : 1) * NVC;
+    base = panel + (s0 * NVC + kr) * ldp + kc;  // this lane's row of the pair's first k-step
+  };
+  auto issue = [&](const double* base, int k, double (&f)[NB]) {
+    const double* rowp = base + (int64_t)(4 * k) * ldp;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) f[b] = __builtin_nontemporal_load(rowp + 16 * b);
+  };
+  auto issue_edge = [&](const double* base, int nrows, int k, double (&f)[NB]) {
     const int r = 4 * k + kr;
     const bool rok = r < nrows;
-    const double* rowp = panel + (s0 * NVC + (rok ? r : 0)) * ldp + kc;
+    const double rs = rok ? 1.0 : 0.0;
+    const double* rowp = base + (int64_t)((rok ? r : kr) - kr) * ldp;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const bool ok = rok && (16 * b + kc < ldp);
-      const double x = __builtin_nontemporal_load(rowp + (ok ? 16 * b : 0));
-      f[b] = ok ? x : 0.0;
-    }
-    if (++ik == KSP) {
-      ik = 0;
-      ++ip;
+      const int c = 16 * b + kc < ldp ? 16 * b : (int)ldp - 1 - kc;
+      f[b] = __builtin_nontemporal_load(rowp + c) * rs;
     }
   };
   auto mma = [&](const double (&f)[NB]) {
@@ -1834,20 +1838,46 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
         ++t;
       }
   };
-  // three units in flight: unit u + 2 is requested while unit u is multiplied
+  // Nine units (k-steps) per pair, three fragment sets in rotation: unit k + 2 is requested while unit k is
+  // multiplied, across pair boundaries (the last two units of pair p request the first two of pair p + 1).  The
+  // pipelined loop runs the workgroup's whole pairs with plain loads; the panel's last pair (the workgroup with
+  // f1 == N) and an odd last sample run after it, unit by unit, with the clamped loads.
+  const int64_t nfull = (f1 - f0) / 2;
+  const int64_t nfast = f1 >= N && nfull > 0 ? nfull - 1 : nfull;
   double fa[NB], fb[NB], fc[NB];
-  if (U > 0) {
-    issue(fa);
-    issue(fb);
+  const double* cb = panel;
+  int cn = 0;
+  if (nfast > 0) {
+    wait_pair(0);
+    pair_base(0, cb, cn);
+    issue(cb, 0, fa);
+    issue(cb, 1, fb);
   }
-  static_assert(KSP % 3 == 0, "whole rounds of three units per pair");
-  for (int64_t u = 0; u < U; u += 3) {
-    issue(fc);
-    mma(fa);
-    issue(fa);
+  for (int64_t p = 0; p < nfast && !bad; ++p) {
+    issue(cb, 2, fc); mma(fa);
+    issue(cb, 3, fa); mma(fb);
+    issue(cb, 4, fb); mma(fc);
+    issue(cb, 5, fc); mma(fa);
+    issue(cb, 6, fa); mma(fb);
+    issue(cb, 7, fb); mma(fc);
+    issue(cb, 8, fc); mma(fa);
+    const bool more = p + 1 < nfast;
+    if (more) {
+      wait_pair(p + 1);
+      pair_base(p + 1, cb, cn);
+      issue(cb, 0, fa);
+    }
     mma(fb);
-    issue(fb);
+    if (more) issue(cb, 1, fb);
     mma(fc);
+  }
+  for (int64_t p = nfast; p < np && !bad; ++p) {
+    wait_pair(p);
+    pair_base(p, cb, cn);
+    for (int k = 0; k < KSP; ++k) {
+      issue_edge(cb, cn, k, fa);
+      mma(fa);
+    }
   }
   double* o = slab + ((size_t)blockIdx.x * K12_NSLOTS + R.base) * 256;
 #pragma unroll
@@ -1878,10 +1908,10 @@ k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, con
                                                  f0, f1);
   } else {
     switch (wave - K1_WAVES) {
-      case 0: k12_gram_wave<0, NVC>(panel, ldp, f0, f1, ready, slab); break;
-      case 1: k12_gram_wave<1, NVC>(panel, ldp, f0, f1, ready, slab); break;
-      case 2: k12_gram_wave<2, NVC>(panel, ldp, f0, f1, ready, slab); break;
-      default: k12_gram_wave<3, NVC>(panel, ldp, f0, f1, ready, slab); break;
+      case 0: k12_gram_wave<0, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
+      case 1: k12_gram_wave<1, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
+      case 2: k12_gram_wave<2, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
+      default: k12_gram_wave<3, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
     }
   }
 }
