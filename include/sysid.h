@@ -231,12 +231,16 @@ int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4);
 /* K2 Gram deal chosen at model creation: {tile columns, tile slots of the f64, f32 and bf16 deals}. */
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
 
-/* Fused K1 + Gram (k12_fused_panel_gram): the full-output f64 path of the quadruped models (nv = 18, a 10-tile
- * Gram: Spot, Solo-12) builds the stacked panel and the Gram in one launch, the Gram waves reading the panel back
- * from L2 while the K1 waves of their workgroup produce it.  Same outputs and contract as
- * sysid_build_device (the Gram differs from the unfused path's only in summation order, ~1e-16 relative).  On by
- * default where supported (environment SYSID_FUSE=0 turns it off at engine creation); sysid_set_fusion switches
- * it per engine; sysid_fused tells whether `flags` (with SYSID_EMIT_GRAM, f64, the engine's panel_ld) run fused. */
+/* Fused K1 + Gram (k12_fused_panel_gram): the f64 paths of the quadruped models (nv = 18, a 10-tile Gram: Spot,
+ * Solo-12) build the projected rows and the Gram in one launch, the Gram waves reading each pair of samples'
+ * rows back from L2 while the K1 waves of their workgroup produce the next ones.  Full outputs
+ * (sysid_build_device with SYSID_EMIT_GRAM and the engine's panel_ld): the stacked panel is written as before.
+ * Gram-only (sysid_build_gram_device, f64, projector rows): the rows go through per-wave rings of three sample
+ * pairs in the workspace (~140 MB, they stay on-die) instead of chunk panels; SYSID_GRAM_NULLSPACE keeps the
+ * unfused nullspace-row path.  Same outputs and contracts (the Gram differs from the unfused path's only in
+ * summation order, ~1e-16 relative).  On by default where supported (environment SYSID_FUSE=0 turns it off at
+ * engine creation); sysid_set_fusion switches it per engine; sysid_fused tells whether `flags` run fused (with a
+ * stacked-output flag: sysid_build_device; without: sysid_build_gram_device). */
 int32_t sysid_set_fusion(sysid_engine* e, int32_t on);
 int32_t sysid_fused(const sysid_engine* e, uint32_t flags);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */

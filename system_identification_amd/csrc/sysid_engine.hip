@@ -261,15 +261,15 @@ bool k12_active(const sysid_engine* e, uint32_t flags, int64_t ld_panel) {
 }
 
 int launch_k12(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
-               double* slab, hipStream_t st) {
+               double* slab, hipStream_t st, int ring = 0) {
   K1Params kp = e->kp;
   const sysid_engine::K1Shape& K = e->k1m[0];
   kp.pov = 0;
   kp.wave_dbl = K.wave_dbl;
   kp.rg = k1_row_groups(kp.NJ, 64 / k1_spw(K.variant));
   kp.out_cols = (int)std::min<int64_t>(ld_panel, e->ldp);
-  sysid_launch::k12_launch(dim3((unsigned)k12_grid(e, N)), e->k12_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel, ld_panel,
-                           slab);
+  sysid_launch::k12_launch(ring, dim3((unsigned)k12_grid(e, N)), e->k12_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
+                           ld_panel, slab);
   HIP_TRY(e, hipGetLastError());
   return SYSID_OK;
 }
@@ -378,11 +378,21 @@ size_t cmp_tail_bytes(const sysid_engine* e, int64_t C) {
   return align256((size_t)C * 4) + align256((size_t)C * e->nv * 4);
 }
 
+// The fused Gram-only form (k12 ring): [K1 counters | slabs | rings]; rings of K12_RING two-sample slots per K1
+// wave, one row of slack for the over-read of the last row (k12_gram_wave).
+size_t k12_ring_bytes(const sysid_engine* e, int64_t N) {
+  return align256(((size_t)k12_grid(e, N) * K1_WAVES * sysid_launch::K12_RING * 2 * e->nv + 1) * e->ldp * sizeof(double));
+}
+size_t k12_ring_ws_bytes(const sysid_engine* e, int64_t N) {
+  return WORK_BYTES + k12_slab_bytes(e, N) + k12_ring_bytes(e, N);
+}
+
 // [K1 counters | row total, segment sums | panel chunk | K2 slabs | row counts | row list]
 size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
   const int64_t C = gram_chunk(e, N, prec), rows = C * e->nv;
-  return WORK_BYTES + cmp_head_bytes(C) + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) +
-         slab_bytes(e, rows, prec) + cmp_tail_bytes(e, C);
+  const size_t chunked = WORK_BYTES + cmp_head_bytes(C) + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) +
+                         slab_bytes(e, rows, prec) + cmp_tail_bytes(e, C);
+  return prec == 0 && e->k12_ok ? std::max(chunked, k12_ring_ws_bytes(e, N)) : chunked;
 }
 
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
@@ -398,6 +408,8 @@ size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every pr
 // 31 of 35 rows anyway) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save).
 int gram_nullspace(const sysid_engine* e, uint32_t flags) {
   const int prec = gram_prec(flags);
+  // the fused Gram-only kernel (f64, quadrupeds) streams the projector rows through its rings
+  if (prec == 0 && e->k12_ok && e->fuse && !(flags & SYSID_GRAM_NULLSPACE)) return 0;
   const bool want_ns = (flags & SYSID_GRAM_NULLSPACE)   ? true
                        : (flags & SYSID_GRAM_PROJECTOR) ? false
                                                         : prec != 2 && !e->k1m[prec].qf;
@@ -413,6 +425,24 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
                    gram_ws_bytes_prec(e, N, prec));
   if (reinterpret_cast<uintptr_t>(d_ws) & 255) return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
+  if (prec == 0 && !cmp && e->k12_ok && e->fuse) {
+    // fused: K1 + Gram over all N in one launch, the rows through per-wave rings that stay on-die; events as the
+    // chunked form's (chunk 0's "K1" = the fused kernel, every other stage 0, then K3)
+    double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
+    double* ring = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + k12_slab_bytes(e, N));
+    size_t k = 0;
+    auto mark = [&]() -> int {
+      if (ev && k < ev->size()) HIP_TRY(e, hipEventRecord((*ev)[k++], st));
+      return SYSID_OK;
+    };
+    int rc;
+    if ((rc = mark())) return rc;
+    if ((rc = launch_k12(e, d_in, N, ld, ring, e->ldp, slab, st, 1))) return rc;
+    while (ev && k + 1 < ev->size())
+      if ((rc = mark())) return rc;
+    if ((rc = launch_k3_tiles(e, (int)k12_grid(e, N), slab, e->d_k12_tiles, K12_NSLOTS, d_gram, st))) return rc;
+    return mark();
+  }
   const int64_t C = gram_chunk(e, N, prec), rows0 = C * e->nv, ldc = gram_ld(e, prec);
   if (rows0 >= ((int64_t)1 << 31)) return set_err(e, SYSID_E_INVALID, "Gram-only chunk of %lld rows", (long long)rows0);
   auto* work = static_cast<unsigned long long*>(d_ws);
@@ -865,11 +895,12 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     // the fused K1 + Gram kernel: the quadruped K1 beside the 10-column Gram waves, one workgroup per CU
     if (e->k1m[0].variant == K1_C4_NV18 && e->ntc == K12_NTC) {
       const size_t lds = (size_t)(MI.ndbl + K1_WAVES * k1_spw(K1_C4_NV18) * e->k1m[0].wave_dbl) * sizeof(double) +
-                         K1_WAVES * sizeof(int);
+                         2 * K1_WAVES * sizeof(int);  // + the ready / consumed counters
       int nb = 0;
       if (lds <= 160 * 1024 &&
-          hipFuncSetAttribute(sysid_launch::k12_fn(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sysid_launch::k12_fn(), 64 * (K1_WAVES + K12_GW), lds) ==
+          hipFuncSetAttribute(sysid_launch::k12_fn(0), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+          hipFuncSetAttribute(sysid_launch::k12_fn(1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sysid_launch::k12_fn(0), 64 * (K1_WAVES + K12_GW), lds) ==
               hipSuccess &&
           nb >= 1) {
         std::vector<int2> tl(K12_NSLOTS);
@@ -1368,7 +1399,9 @@ int32_t sysid_set_fusion(sysid_engine* e, int32_t on) {
 
 int32_t sysid_fused(const sysid_engine* e, uint32_t flags) {
   if (!e) return SYSID_E_INVALID;
-  return k12_active(e, flags | SYSID_EMIT_GRAM, e->ldp) ? 1 : 0;
+  if (flags & (SYSID_EMIT_Y | SYSID_EMIT_TAU | SYSID_EMIT_FRICTION))
+    return k12_active(e, flags | SYSID_EMIT_GRAM, e->ldp) ? 1 : 0;
+  return gram_prec(flags) == 0 && e->k12_ok && e->fuse && !gram_nullspace(e, flags) ? 1 : 0;  // Gram-only
 }
 
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4) {

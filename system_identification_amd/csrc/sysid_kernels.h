@@ -22,6 +22,7 @@ constexpr int JT_FREEFLYER = 1;
 constexpr int JT_REVOLUTE = 2;
 constexpr int K1_WAVES = 4;            // waves (= samples in flight) per K1 workgroup
 constexpr int K1_SHARDS = 8;           // K1 sample ranges / claim counters (one per XCD), 128 B apart
+constexpr int K12_GW = 4;              // Gram waves per fused K1 + Gram workgroup (k12_fused_panel_gram)
 
 // ------------------------------------------------------------------------------------------------
 // layouts shared by host and device
@@ -492,12 +493,15 @@ constexpr int K1_QF_KMAX = 6;
 // counters) and the K1 waves of the fused kernel (k12_fused_panel_gram, FUSED = 1: the workgroup's sample range
 // [f0, f1) dealt statically, wave w taking steps w, w + K1_WAVES, ...; after each step's panel stores have
 // completed the wave publishes its step count in k12_ready[w] (LDS) for the Gram waves of its workgroup).
+// FUSED = 2 (the fused Gram-only mode): `panel` is the wave's ring of k12_ring steps; step t's rows go to slot
+// t % k12_ring once the Gram waves have counted (k12_consumed[w]) their loads of step t - k12_ring.
 template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0, int FUSED = 0>
 __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __restrict__ mimg_g,
                                         const double* __restrict__ in, int64_t N, int64_t ld,
                                         OutT* __restrict__ panel, int64_t ldp, unsigned long long* __restrict__ work,
                                         double* __restrict__ dbg, int* __restrict__ rcount, int* k12_ready,
-                                        int64_t f0, int64_t f1) {
+                                        int64_t f0, int64_t f1, const int* k12_consumed = nullptr,
+                                        int k12_ring = 0) {
   static_assert(!(POV && CMP), "the nullspace mode runs the plain layout");
   static_assert(!QF || (NVC == 0 && !POV && !CMP), "the Q-form is a runtime-nv, plain-layout kernel");
   static_assert(!FUSED || (!CMP && !POV && !QF), "the fused kernel runs the plain projector-row layout");
@@ -1301,12 +1305,23 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     // for: publishing them here costs no extra wait
     if (steps_done > 0) publish(steps_done);
 
+    if constexpr (FUSED == 2) {
+      // the ring slot this step overwrites was step steps_done - k12_ring: every Gram wave has loaded it
+      const int need = (steps_done - k12_ring + 1) * K12_GW;
+      int spins = 0;
+      while (need > 0 && __hip_atomic_load(k12_consumed + wave, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need &&
+             ++spins < (1 << 23))  // ~1 s bound: a bug must not hang the device (the Gram waves poison theirs)
+        __builtin_amdgcn_s_sleep(2);
+    }
     __builtin_amdgcn_s_setprio(0);
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
     // One G row (6 + 6*chain FMAs) feeds 42 FMAs.
-    OutT* out = panel + ((s + half) * nv) * ldp;
+    // the step's rows: the stacked panel's, or (fused Gram-only) the ring slot of this step
+    OutT* const obase = FUSED == 2 ? panel + (int64_t)((steps_done % (k12_ring > 0 ? k12_ring : 1)) * SPW) * nv * ldp
+                                   : panel + s * nv * ldp;
+    OutT* out = obase + (int64_t)half * nv * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
     auto block_row = [&](int r, const double* F, const int* dof, int cl, double* y) {
       const double* h = h1_in_p ? Ps + r * nv + kp.ff0 : H1 + 6 * r;
@@ -1393,7 +1408,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       // 2x, plus dg for the second group.  The row start of the wave's first sample is wave-uniform (scalar
       // registers); the second sample's rows and the column go into a 32-bit lane byte offset, so each store is
       // a scalar-base + lane-offset store with no 64-bit address math.
-      char* ybase = reinterpret_cast<char*>(panel + (s * NVC) * ldp);
+      char* ybase = reinterpret_cast<char*>(obase);
       const uint32_t yhoff = (uint32_t)(half * NVC * (int)ldp * (int)sizeof(OutT));
       const int dg = rh * (int)ldp - kp.wy;
       // Rows in pairs with two explicit H1 / P register sets (no copies between them): row rho + 1's LDS reads
@@ -1747,7 +1762,6 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 // deadlock; a wait still gives up after ~1 s and poisons its tiles with NaN (a bug must not hang the GPU).
 // ------------------------------------------------------------------------------------------------
 constexpr int K12_NTC = 10;
-constexpr int K12_GW = 4;        // Gram waves per workgroup (waves 4..7: one per SIMD)
 constexpr int K12_NSLOTS = 55;   // upper tiles of a 10 x 10 tile Gram
 struct K12Role {
   int nc;        // tile columns of the role
@@ -1775,9 +1789,12 @@ __host__ __device__ constexpr int2 k12_tile(int slot) {
   return int2{-1, -1};
 }
 
-template <int W, int NVC>
+// RING = 0: the pairs are rows of the stacked panel; RING > 0 (fused Gram-only): pair p of the workgroup is slot
+// (p / 4) % RING of K1 wave p % 4's ring, and its loads are counted in k12_consumed[p % 4] once complete.
+template <int W, int NVC, int RING>
 __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, int64_t ldp, int64_t N, int64_t f0,
-                                              int64_t f1, const int* k12_ready, double* __restrict__ slab) {
+                                              int64_t f1, const int* k12_ready, double* __restrict__ slab,
+                                              int* k12_consumed) {
   constexpr K12Role R = k12_role(W);
   constexpr int NB = R.col[0] + 1;         // fragment blocks 0 .. col[0] (every role's first column is its widest)
   constexpr int NT = R.ntiles;
@@ -1810,7 +1827,22 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
   auto pair_base = [&](int64_t p, const double*& base, int& nrows) {
     const int64_t s0 = f0 + 2 * p;
     nrows = (f1 - s0 >= 2 ? 2 : 1) * NVC;
-    base = panel + (s0 * NVC + kr) * ldp + kc;  // this lane's row of the pair's first k-step
+    if constexpr (RING > 0) {
+      const int64_t slot = ((int64_t)blockIdx.x * K1_WAVES + (p & (K1_WAVES - 1))) * RING + (p / K1_WAVES) % RING;
+      base = panel + (slot * 2 * NVC + kr) * ldp + kc;
+    } else {
+      base = panel + (s0 * NVC + kr) * ldp + kc;  // this lane's row of the pair's first k-step
+    }
+  };
+  // ring mode: pair p's loads have all returned (the ones issued after them: `younger`) -> its slot may be reused
+  auto consumed = [&](int64_t p, auto younger) {
+    if constexpr (RING > 0) {
+      constexpr int Y = decltype(younger)::value;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Y) : "memory");
+      if (lane == 0) __hip_atomic_fetch_add(k12_consumed + (p & (K1_WAVES - 1)), 1, __ATOMIC_RELEASE,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    (void)p;
   };
   auto issue = [&](const double* base, int k, double (&f)[NB]) {
     const double* rowp = base + (int64_t)(4 * k) * ldp;
@@ -1870,6 +1902,8 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
     mma(fb);
     if (more) issue(cb, 1, fb);
     mma(fc);
+    if (more) consumed(p, std::integral_constant<int, 2 * NB>{});
+    else consumed(p, std::integral_constant<int, 0>{});
   }
   for (int64_t p = nfast; p < np && !bad; ++p) {
     wait_pair(p);
@@ -1878,6 +1912,7 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
       issue_edge(cb, cn, k, fa);
       mma(fa);
     }
+    consumed(p, std::integral_constant<int, 0>{});
   }
   double* o = slab + ((size_t)blockIdx.x * K12_NSLOTS + R.base) * 256;
 #pragma unroll
@@ -1886,17 +1921,20 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
     for (int j = 0; j < 4; ++j) o[t * 256 + (kr + 4 * j) * 16 + kc] = bad ? __builtin_nan("") : acc[t][j];
 }
 
-template <int MAXCH, int NVC, int SPW>
+// RING = 0: full outputs (`panel` = the stacked panel); RING > 0: Gram-only (`panel` = the rings, gridDim.x x
+// K1_WAVES x RING slots of 2 nv rows, plus one row of slack for the last row's over-read).
+template <int MAXCH, int NVC, int SPW, int RING>
 __global__ void __launch_bounds__(64 * (K1_WAVES + K12_GW), 2)
 k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
                      int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp, double* __restrict__ slab) {
   static_assert(NVC == 18 && SPW == 2, "the fused kernel serves the quadruped K1 (two samples per wave)");
   extern __shared__ double smem[];
   int* ready = reinterpret_cast<int*>(smem + kp.mimg_dbl + K1_WAVES * SPW * kp.wave_dbl);
+  int* consumed = ready + K1_WAVES;
   {
     uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
     for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
-    if (threadIdx.x < K1_WAVES) ready[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * K1_WAVES) ready[threadIdx.x] = 0;  // ready[4], consumed[4]
   }
   __syncthreads();
   const int64_t P = (N + SPW - 1) / SPW;
@@ -1904,14 +1942,20 @@ k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, con
   const int64_t f0 = p0 * SPW, f1 = p1 * SPW < N ? p1 * SPW : N;
   const int wave = threadIdx.x >> 6;
   if (wave < K1_WAVES) {
-    k1_body<MAXCH, NVC, SPW, double, 0, 0, 0, 1>(kp, mimg_g, in, N, ld, panel, ldp, nullptr, nullptr, nullptr, ready,
-                                                 f0, f1);
+    if constexpr (RING > 0) {
+      double* ring = panel + ((int64_t)blockIdx.x * K1_WAVES + wave) * RING * SPW * NVC * ldp;
+      k1_body<MAXCH, NVC, SPW, double, 0, 0, 0, 2>(kp, mimg_g, in, N, ld, ring, ldp, nullptr, nullptr, nullptr, ready,
+                                                   f0, f1, consumed, RING);
+    } else {
+      k1_body<MAXCH, NVC, SPW, double, 0, 0, 0, 1>(kp, mimg_g, in, N, ld, panel, ldp, nullptr, nullptr, nullptr,
+                                                   ready, f0, f1);
+    }
   } else {
     switch (wave - K1_WAVES) {
-      case 0: k12_gram_wave<0, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
-      case 1: k12_gram_wave<1, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
-      case 2: k12_gram_wave<2, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
-      default: k12_gram_wave<3, NVC>(panel, ldp, N, f0, f1, ready, slab); break;
+      case 0: k12_gram_wave<0, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
+      case 1: k12_gram_wave<1, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
+      case 2: k12_gram_wave<2, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
+      default: k12_gram_wave<3, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
     }
   }
 }

@@ -89,3 +89,36 @@ def test_fused_bitwise_repeatable_and_graph_replay():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(bufs["gram"], G) and torch.equal(bufs["panel"], P)
+
+
+@pytest.mark.parametrize("robot,N", [("spot", 1), ("spot", 7), ("spot", 513), ("spot", 20000), ("spot", 100001),
+                                     ("solo12", 3001)])
+def test_fused_gram_only_ring(robot, N):
+    """The fused Gram-only form (rows through per-wave rings of three sample pairs, never a panel): against the
+    full-output fused Gram (the same rows, the same summation order: bitwise), the unfused nullspace-row path
+    (1e-10) and the C oracle (1e-6, whole N); bitwise repeatable."""
+    import torch
+    from system_identification_amd.engine import EMIT_GRAM
+    model = load_robot(robot)
+    e = Engine(model)
+    assert e.fused(EMIT_GRAM) and e.gram_rows("f64") == "projector"
+    d = generate(model, N, config_index=7)
+    din = torch.from_numpy(channel_block(d)).cuda()
+
+    def gram_only(rows="auto"):
+        b = e.alloc_gram_device(N)
+        b["gram"].fill_(float("nan"))
+        e.build_gram_device(din, N, b, precision="f64", rows=rows)
+        torch.cuda.synchronize()
+        return b["gram"].cpu().numpy()
+    G = gram_only()
+    assert np.all(np.isfinite(G)) and np.array_equal(G, G.T)
+    assert np.array_equal(G, gram_only())
+    _, Gfull = run(e, d, N, True)
+    assert np.array_equal(G, Gfull)  # same rows, same deal, same order
+    Gz = gram_only("nullspace")
+    assert rel(G, Gz) <= 1e-10, rel(G, Gz)
+    o = COracle(model).build(*[d[k] for k in CH], nthreads=16, stacked=False)
+    W = e.w
+    assert rel(G[:W, :W], o["gram"]) < 1e-6 and rel(G[:W, W], o["Atb"]) < 1e-6
+    assert abs(G[W, W] - o["btb"]) <= 1e-6 * abs(o["btb"])
