@@ -376,7 +376,13 @@ def main():
     # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only: the chunked
     # path itself, each stage summed over its chunks.
     n_time = N
+    fused = eng.fused(tflags & ~0x7 if args.gram_only else flags)  # K12: K1 + Gram in one launch (ms[1] = 0)
     ms = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
+    ms_unfused = None
+    if fused:  # the same stages with fusion off, for the record (K1 -> K2 -> K3 as three launches)
+        eng.set_fusion(False)
+        ms_unfused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
+        eng.set_fusion(True)
     nv, W = model.nv, eng.w
     in_b = (model.nq + 2 * nv + model.nj + model.n_ee) * 8
     esize = {"f64": 8, "f32": 4, "bf16": 2}[args.precision] if args.gram_only else 8
@@ -384,7 +390,7 @@ def main():
     bytes_k1 = in_b + panel_b                                                       # SURVEY §8d per sample
     flops_k2 = nv * W * (W + 1) + 2 * nv * W                                       # SYRK + Aᵀb per sample
     k1_gbs = n_time * bytes_k1 / (ms[0] * 1e-3) / 1e9
-    k2_tfs = n_time * flops_k2 / (ms[1] * 1e-3) / 1e12
+    k2_tfs = n_time * flops_k2 / (ms[1] * 1e-3) / 1e12 if ms[1] > 0 else 0.0
     rows_per_sample = float(nv)
     if args.gram_only and rows_used == "nullspace" and 3 * model.n_ee <= 12:
         # the Gram kernel's own work: nv - rank(J_c) rows per sample (rank 3 per foot in contact: the synthetic
@@ -392,7 +398,23 @@ def main():
         # nv-row count stays in K2_TFps / gram_gflops
         rows_per_sample = float(np.mean(nv - 3 * (data["contact"] != 0).sum(axis=0)))
     k2_exec_tfs = k2_tfs * rows_per_sample / nv
-    if ms[0] >= ms[1]:
+    if fused:
+        # the fused kernel does K1's HBM work and the Gram's MFMA work in one launch; the MFMA side is its floor
+        # (Spot 20k: 8.70 GFLOP at 78.6 TF/s = 0.111 ms against 458 MB of HBM writes at 8 TB/s = 0.057 ms)
+        traffic, src = pmc_traffic("k12_fused_panel_gram", args.robot, N)
+        peak = MFMA_PEAK_TFS["f64"]
+        k12_tfs = n_time * flops_k2 / (ms[0] * 1e-3) / 1e12
+        hbm_b = n_time * (in_b + (0 if args.gram_only else panel_b))
+        roof = {"kernel": "k12_fused_panel_gram", "bound": "mfma", "achieved": round(k12_tfs, 3), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(k12_tfs / peak, 4), "traffic": traffic, "traffic_source": src,
+                "algorithmic_flops_per_launch": round(n_time * flops_k2),
+                "algorithmic_hbm_bytes_per_launch": hbm_b,
+                "hbm_achieved_GBps": round(hbm_b / (ms[0] * 1e-3) / 1e9, 1),
+                "avg_launch_ms": round(ms[0], 5),
+                "note": "K1 (regressor + projector rows) and K2 (Gram MFMA) in one launch, the rows re-read from "
+                        "L2, not HBM" + ("; Gram-only: the rows never reach HBM (per-wave rings)" if args.gram_only
+                                         else "")}
+    elif ms[0] >= ms[1]:
         traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N) if not args.gram_only else (None, None)
         roof = {"kernel": "k1_regressor_panel", "bound": "hbm", "achieved": round(k1_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
@@ -417,7 +439,7 @@ def main():
                   "source": "HIP events on the launch stream between consecutive timed steps (rank 0)"}
     # step-level floor: the bytes the step must move (inputs + panel written by K1 and read back by K2; Gram-only
     # chunks may stay on-die and are not counted) at HBM peak, and the Gram flops at the MFMA peak
-    step_bytes = N * (in_b + (0 if args.gram_only else 2 * panel_b))
+    step_bytes = N * (in_b + (0 if args.gram_only else (1 if fused else 2) * panel_b))
     hbm_floor = step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
     mfma_floor = N * flops_k2 / (MFMA_PEAK_TFS[args.precision if args.gram_only else "f64"] * 1e12) * 1e3
     value = total_per_step * args.steps / elapsed
@@ -431,22 +453,30 @@ def main():
                 "inverse-dynamics torques + noise, trot contacts with LOST=2); no .dat ships with the reference",
         "config": {"workload": f"{args.robot} " + (f"{args.total_samples} samples split over {world} GPU(s)" if strong
                                                     else f"{N} samples per GPU") + ", " + (
-                       f"Gram only ({rows_used} rows chunked on the device, {args.precision} Gram)" if args.gram_only else
+                       (f"Gram only ({rows_used} rows through the fused kernel's on-die rings, {args.precision} Gram)"
+                        if fused else f"Gram only ({rows_used} rows chunked on the device, {args.precision} Gram)")
+                       if args.gram_only else
                        "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
                    "robot": args.robot, "samples_per_gpu": N, "total_samples_per_step": total_per_step,
                    "nv": nv, "W": W, "parallelism": f"dp{world}",
                    "exchange": exchange_name,
                    "exchange_check": exchange_check,
-                   "timed_region": ("K1 + K2 per panel chunk + K3 (Gram-only)" if args.gram_only else "K1 + K2 + K3")
+                   "timed_region": (("fused K1 + Gram (K12) + K3" + (" (Gram-only)" if args.gram_only else "")) if fused
+                                    else "K1 + K2 per panel chunk + K3 (Gram-only)" if args.gram_only else "K1 + K2 + K3")
                    + ", HBM-resident inputs and outputs" + (", + the Gram all-reduce" if comm is not None or world > 1
                                                              else "")},
         "step_times": step_stats,
         "settle": settle,
         "steady_state": steady,
         "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
-        "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
-                      "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},
-        "K1_GBps": round(k1_gbs, 1), "K2_TFps": round(k2_tfs, 3),
+        "kernel_ms": ({"K12_fused_panel_gram": round(ms[0], 5), "K3_gram_reduce": round(ms[2], 5),
+                       "samples_timed": n_time} if fused else
+                      {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
+                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time}),
+        "kernel_ms_unfused": None if ms_unfused is None else {
+            "K1_regressor_panel": round(ms_unfused[0], 5), "K2_gram_syrk": round(ms_unfused[1], 5),
+            "K3_gram_reduce": round(ms_unfused[2], 5), "note": "the same step with fusion off (sysid_set_fusion)"},
+        "K1_GBps": None if fused else round(k1_gbs, 1), "K2_TFps": None if fused else round(k2_tfs, 3),
         "roofline": roof,
         "step_roofline": {"hbm_bytes": step_bytes, "hbm_floor_ms": round(hbm_floor, 5),
                           "mfma_floor_ms": round(mfma_floor, 5), "floor_ms": round(max(hbm_floor, mfma_floor), 5),
