@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sysid.h"
@@ -84,6 +86,8 @@ struct sysid_engine {
   size_t out_cap = 0;
   int host_register = -1;    // host API copies: 1 page-lock the caller's arrays, 0 pageable, -1 by size
   double* d_dump = nullptr;  // diagnostics only
+  double* h_stage = nullptr;  // host API: page-locked staging of the input block (grow-only)
+  size_t h_stage_cap = 0;
   std::string err;
 };
 
@@ -523,6 +527,55 @@ int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemc
   return SYSID_OK;
 }
 
+// Host entry points: the caller's channel arrays (pageable numpy memory) -> the device input block, at DMA speed.
+// A pageable copy runs at the speed of the runtime's single staging memcpy (Spot 20k: 11.4 MB at ~17 GB/s, the
+// largest part of the Gram-only e2e step).  Here host threads pack the channels into the engine's page-locked
+// staging block chunk by chunk (samples [c0, c1) of every channel) and each finished chunk leaves as one 2-D DMA
+// while the threads pack the next, so the copy engine runs at PCIe rate beside the packing.  Returns with every
+// chunk enqueued on `st` (the staging block is reused by the next call only after that call's stream sync).
+int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, int nsrc, int64_t N, int64_t ld,
+                 double* d_dst, hipStream_t st) {
+  const size_t need = (size_t)e->in_rows * N * sizeof(double);
+  if (need > e->h_stage_cap) {
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    e->h_stage = nullptr;
+    e->h_stage_cap = 0;
+    HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
+    e->h_stage_cap = need;
+  }
+  std::vector<const double*> row_src;  // channel row r of the block <- its source row
+  for (int k = 0; k < nsrc; ++k)
+    for (int r = 0; r < nrows[k]; ++r) row_src.push_back(srcs[k] + (int64_t)r * ld);
+  const int R = (int)row_src.size();
+  int T = 8;
+  if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
+  T = std::max(1, std::min(T, R));
+  const int64_t CH = std::max<int64_t>(4096, (N + 7) / 8);  // samples per chunk
+  const int nch = (int)((N + CH - 1) / CH);
+  std::vector<std::atomic<int>> done(nch);
+  for (auto& d : done) d.store(0);
+  std::vector<std::thread> pool;
+  double* hs = e->h_stage;
+  for (int t = 0; t < T; ++t)
+    pool.emplace_back([&, t]() {
+      for (int c = 0; c < nch; ++c) {
+        const int64_t c0 = c * CH, n = std::min(CH, N - c0);
+        for (int r = t; r < R; r += T) std::memcpy(hs + (int64_t)r * N + c0, row_src[r] + c0, (size_t)n * sizeof(double));
+        done[c].fetch_add(1, std::memory_order_release);
+      }
+    });
+  int rc = SYSID_OK;
+  for (int c = 0; c < nch; ++c) {
+    while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    const int64_t c0 = c * CH, n = std::min(CH, N - c0);
+    if (rc == SYSID_OK && hipMemcpy2DAsync(d_dst + c0, (size_t)N * sizeof(double), hs + c0, (size_t)N * sizeof(double),
+                                           (size_t)n * sizeof(double), R, hipMemcpyHostToDevice, st) != hipSuccess)
+      rc = set_err(e, SYSID_E_DEVICE, "input copy failed");
+  }
+  for (auto& th : pool) th.join();
+  return rc;
+}
+
 int host_unregister(sysid_engine* e, std::vector<void*>& registered) {
   for (void* p : registered) (void)hipHostUnregister(p);
   registered.clear();
@@ -931,6 +984,7 @@ void sysid_destroy(sysid_engine* e) {
   for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_k12_tiles, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
+  if (e->h_stage) (void)hipHostFree(e->h_stage);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1222,11 +1276,14 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   hipStream_t st = e->stream;
   std::vector<void*> reg;
   auto fail = [&](int code) { (void)hipStreamSynchronize(st); host_unregister(e, reg); return code; };
-  // inputs: channel c of the caller's arrays -> row c of the device block (one copy per array when ld == N)
+  // inputs: channel c of the caller's arrays -> row c of the device block: staged through page-locked memory by
+  // host threads for blocks of 1 MiB and more (stage_inputs), else one copy per array
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
+  const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
+  if (staged && (rc = stage_inputs(e, srcs, nrows, 5, N, ld, e->d_in, st)) != SYSID_OK) return fail(rc);
   int64_t r0 = 0;
-  for (int k = 0; k < 5; ++k) {
+  for (int k = 0; k < 5 && !staged; ++k) {
     if (nrows[k] > 0) {
       if (ld == N) {
         if ((rc = host_copy(e, e->d_in + r0 * N, srcs[k], (size_t)nrows[k] * N * sizeof(double),
