@@ -85,7 +85,7 @@ constexpr int BODY_STRIDE = 26;
 //     doubles per sample, so one workgroup of 8 one-sample waves fits a CU's 160 KB (was 3 x 2 waves).
 constexpr int K1_POV_BUF = 12;  // P passes (of 64 entries) a P overlay may hold in registers
 struct WLay {
-  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, dqs, Z, total;
+  int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, dqs, Z, q32, total;
 };
 
 //   * with `nop` (the Q-form kernels, which never form P) there is no P slot at all.
@@ -118,9 +118,13 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc,
   l.Z = u0;                     // Q^T (orthonormal rows of J_c's row space), row r at r * 3 nc (W, Pt, pf
                                 // are dead by then)
   grow(u0 + r2(k * nv > k * k ? k * nv : k * k));
+  l.q32 = 0;
   if (nop) {
     l.P = l.Jc;                 // unused
     l.H1 = D;                   // unused
+    // f32 copies of every row's Q entries (8, zero past k) and motion axis (6) for the bf16 row loop: converted
+    // once per sample instead of by every lane on every row
+    l.q32 = take(nv * 7);
     l.total = o;
     return l;
   }
@@ -1479,6 +1483,14 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       // specialised for k <= 3 and k <= 6.
       const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);
       const int nyh = 2 * nbody;  // even: both lanes of a pair are always active together
+      if constexpr (std::is_same_v<OutT, __bf16>) {
+        float* q32w = reinterpret_cast<float*>(wr + L.q32);
+        for (int e2 = hl; e2 < nv * 14; e2 += HW) {
+          const int r = e2 / 14, c = e2 - 14 * r;
+          q32w[e2] = c < 8 ? (c < K1_QF_KMAX ? (float)Qt[r * K1_QF_KMAX + c] : 0.0f) : (float)Jws[6 * r + c - 8];
+        }
+        wsync();
+      }
       for (int it = hl; it < nyh && valid; it += HW) {
         const int i = (it >> 1) + 1, h = it & 1, c3 = 3 * h;
         // K (this lane's three columns) first, F is not live yet; the chain in a rolled loop
@@ -1568,6 +1580,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         // (v_pk_fma_f32: two FMAs per instruction at the cost of one f64 FMA).  G and the block's outputs carry
         // ~1e-7 relative error, far below the bf16 rounding (2^-9) the panel gets anyway; K and F6 are formed in
         // f64 and rounded once.
+        const float* q32 = reinterpret_cast<const float*>(wr + L.q32);  // [r][Q 0..7 | J 0..5]
         auto rows_f32 = [&](auto kqc) {
           constexpr int KQ = decltype(kqc)::value;
           f32x2_t K01[KQ];
@@ -1585,17 +1598,13 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
 #pragma unroll 1
           for (int r = 0; r < nrows; ++r) {
             const float sf = ((smask >> r) & 1ull) ? 1.0f : 0.0f;
-            const double* jr = jrs + 6 * r;
-            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
+            const float* qrow = q32 + 14 * r;
             float qr[K1_QF_KMAX];
 #pragma unroll
-            for (int j = 0; j < (KQ + 1) / 2; ++j) {
-              const double2 v = q2[j];
-              qr[2 * j] = (float)v.x;
-              qr[2 * j + 1] = (float)v.y;
-            }
-            f32x2_t g01 = f32x2_t{sf * (float)jr[0], sf * (float)jr[1]};
-            float g2 = sf * (float)jr[2];
+            for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = qrow[j];
+            const float* jr = qrow + 8 + c3;
+            f32x2_t g01 = f32x2_t{sf * jr[0], sf * jr[1]};
+            float g2 = sf * jr[2];
 #pragma unroll
             for (int j = 0; j < KQ; ++j) {
               g01 -= qr[j] * K01[j];
