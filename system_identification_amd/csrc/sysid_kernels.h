@@ -1687,6 +1687,23 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
           for (int j = 0; j < K1_QF_KMAX; ++j)
 #pragma unroll
             for (int u = 0; u < 2; ++u) qc[j][u] = Qt[(bd + jc[u]) * K1_QF_KMAX + j];  // zero past k
+          if constexpr (std::is_same_v<OutT, __bf16>) {
+            // bf16 chunk panels: the same in packed f32 from the per-sample f32 rows (q32, made by the Y phase)
+            const float* q32 = reinterpret_cast<const float*>(wr + L.q32);
+            f32x2_t qc2[K1_QF_KMAX];
+#pragma unroll
+            for (int j = 0; j < K1_QF_KMAX; ++j) qc2[j] = f32x2_t{(float)qc[j][0], (float)qc[j][1]};
+            const f32x2_t sc2 = f32x2_t{fcol[0] ? (float)sc[0] : 0.0f, fcol[1] ? (float)sc[1] : 0.0f};
+            for (int r = fg; r < nrows; r += NG, po += pstep) {
+              f32x2_t pe = f32x2_t{r == bd + jc[0] ? 1.0f : 0.0f, r == bd + jc[1] ? 1.0f : 0.0f};
+              const float* qrow = q32 + 14 * r;
+#pragma unroll
+              for (int j = 0; j < K1_QF_KMAX; ++j) pe -= qrow[j] * qc2[j];
+              const float t = (float)tps[r];
+              pe *= sc2;
+              panel_store_f32(reinterpret_cast<__bf16*>(po), tcol[0] ? t : pe.x, tcol[1] ? t : pe.y);
+            }
+          } else {
           for (int r = fg; r < nrows; r += NG, po += pstep) {
             double pe[2] = {r == bd + jc[0] ? 1.0 : 0.0, r == bd + jc[1] ? 1.0 : 0.0};
             const double* qrow = Qt + r * K1_QF_KMAX;
@@ -1701,6 +1718,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
 #pragma unroll
             for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pe[u] * sc[u] : (tcol[u] ? t : 0.0);
             panel_store(po, v2[0], v2[1]);
+          }
           }
         } else {
           for (int r = fg; r < nrows; r += NG, po += pstep) {
