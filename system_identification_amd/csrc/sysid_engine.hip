@@ -14,6 +14,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -39,6 +42,66 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // stream right before each K1 launch, so launches are independent of each other: an aborted launch leaves
 // nothing behind, and launches on different streams with different workspaces may run concurrently.
 constexpr size_t WORK_BYTES = 128 * K1_SHARDS;  // one 128-byte line per claim counter
+
+// A persistent pool of host threads for the host entry points' input packing (stage_inputs): started on first use,
+// joined by sysid_destroy.  run(f) calls f(t) on every worker t and returns when all have finished.
+class HostPool {
+ public:
+  explicit HostPool(int n) : n_(n) {
+    for (int t = 0; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  int size() const { return n_; }
+  // starts f on every worker and returns at once; wait() blocks until all have finished
+  void start(std::function<void(int)> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = std::move(f);
+      pending_ = n_;
+      ++gen_;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [this] { return pending_ == 0; });
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(int)> f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      f(t);
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (--pending_ == 0) done_cv_.notify_all();
+      }
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(int)> job_;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
 
 }  // namespace
 
@@ -88,6 +151,7 @@ struct sysid_engine {
   double* d_dump = nullptr;  // diagnostics only
   double* h_stage = nullptr;  // host API: page-locked staging of the input block (grow-only)
   size_t h_stage_cap = 0;
+  HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
   std::string err;
 };
 
@@ -547,23 +611,24 @@ int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, i
   for (int k = 0; k < nsrc; ++k)
     for (int r = 0; r < nrows[k]; ++r) row_src.push_back(srcs[k] + (int64_t)r * ld);
   const int R = (int)row_src.size();
-  int T = 8;
-  if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
-  T = std::max(1, std::min(T, R));
+  if (!e->pool) {
+    int T = 8;  // the GPU box grants a job 16 host threads (OMP_NUM_THREADS): half of them pack
+    if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
+    e->pool = new HostPool(T);
+  }
+  const int T = e->pool->size();
   const int64_t CH = std::max<int64_t>(4096, (N + 7) / 8);  // samples per chunk
   const int nch = (int)((N + CH - 1) / CH);
   std::vector<std::atomic<int>> done(nch);
   for (auto& d : done) d.store(0);
-  std::vector<std::thread> pool;
   double* hs = e->h_stage;
-  for (int t = 0; t < T; ++t)
-    pool.emplace_back([&, t]() {
-      for (int c = 0; c < nch; ++c) {
-        const int64_t c0 = c * CH, n = std::min(CH, N - c0);
-        for (int r = t; r < R; r += T) std::memcpy(hs + (int64_t)r * N + c0, row_src[r] + c0, (size_t)n * sizeof(double));
-        done[c].fetch_add(1, std::memory_order_release);
-      }
-    });
+  e->pool->start([&](int t) {
+    for (int c = 0; c < nch; ++c) {
+      const int64_t c0 = c * CH, n = std::min(CH, N - c0);
+      for (int r = t; r < R; r += T) std::memcpy(hs + (int64_t)r * N + c0, row_src[r] + c0, (size_t)n * sizeof(double));
+      done[c].fetch_add(1, std::memory_order_release);
+    }
+  });
   int rc = SYSID_OK;
   for (int c = 0; c < nch; ++c) {
     while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
@@ -572,7 +637,7 @@ int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, i
                                            (size_t)n * sizeof(double), R, hipMemcpyHostToDevice, st) != hipSuccess)
       rc = set_err(e, SYSID_E_DEVICE, "input copy failed");
   }
-  for (auto& th : pool) th.join();
+  e->pool->wait();
   return rc;
 }
 
@@ -985,6 +1050,7 @@ void sysid_destroy(sysid_engine* e) {
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
+  delete e->pool;
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
