@@ -102,6 +102,8 @@ def load_library(path: str = LIB_PATH):
             "g.build()'`).  There is no CPU fallback.")
     lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
+        if os.environ.get("SYSID_LIB") and not hasattr(lib, name):
+            continue  # an older A/B build (SYSID_LIB): its missing entry points stay undeclared
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -385,7 +387,10 @@ class Engine:
         self._check(self.lib.sysid_set_fusion(self._h, 1 if on else 0))
 
     def fused(self, flags: int = EMIT_ALL) -> bool:
-        """Whether build_device with these flags (and the engine's panel ld) runs the fused K1 + Gram kernel."""
+        """Whether these flags run the fused K1 + Gram kernel: with a stacked-output flag build_device (and the
+        engine's panel ld), without one build_gram_device."""
+        if not hasattr(self.lib, "sysid_fused"):
+            return False  # an older A/B build
         return self.lib.sysid_fused(self._h, int(flags)) == 1
 
     def gram_rows(self, precision: str = "f64", rows: str = "auto") -> str:

@@ -15,6 +15,11 @@ for i in 1 2; do
   echo "== unfused (SYSID_FUSE=0)"
   SYSID_FUSE=0 timeout -k 10 120 python tools/quick_time.py spot 20000 2>&1 | grep -v amdgpu.ids || exit 1
 done
+for lib in tools/_libs/base_r03.so system_identification_amd/libsysid.so; do
+  echo "== gram-only $lib"
+  SYSID_LIB=$PWD/$lib timeout -k 10 200 python tools/gram_only_time.py spot 20000 f64 3 2>&1 | grep -v amdgpu.ids || exit 1
+  SYSID_LIB=$PWD/$lib timeout -k 10 200 python tools/gram_only_time.py g1_29dof 125000 bf16 2 2>&1 | grep -v amdgpu.ids || exit 1
+done
 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --exchange-world1 --no-cpu-baseline --no-e2e --no-steady-state > $OUT/bench_xchg.json 2> $OUT/bench_xchg.err || { echo "xchg bench failed"; tail -20 $OUT/bench_xchg.err; exit 1; }
 python -c "import json; d=json.loads(open('$OUT/bench_xchg.json').read().strip().splitlines()[-1]); print(d['config']['exchange'], d['config']['exchange_check'], d['ms_per_step'])"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_driver.json 2> $OUT/bench_driver.err || { echo "bench failed"; tail -20 $OUT/bench_driver.err; exit 1; }

@@ -19,7 +19,11 @@ print(robot, N, "ms per kernel [K1, K2, K3]:", ["%.4f" % x for x in ms], "total 
 bytes_k1 = N * ((m.nq + 2 * m.nv + m.nj + m.n_ee) * 8 + m.nv * (eng.w + 1) * 8)
 W = eng.w
 flops_k2 = N * (m.nv * W * (W + 1) + 2 * m.nv * W)
-print("K1 %.1f GB/s   K2 %.2f TF/s   samples/s %.3e" % (bytes_k1 / ms[0] / 1e6, flops_k2 / ms[1] / 1e9, N / sum(ms) * 1e3))
+if ms[1] > 0:
+    print("K1 %.1f GB/s   K2 %.2f TF/s   samples/s %.3e" % (bytes_k1 / ms[0] / 1e6, flops_k2 / ms[1] / 1e9, N / sum(ms) * 1e3))
+else:  # fused K1 + Gram (ms[0] = the fused kernel)
+    print("fused K12 %.2f TF/s (Gram flops), %.1f GB/s (K1 bytes)   samples/s %.3e" % (
+        flops_k2 / ms[0] / 1e9, bytes_k1 / ms[0] / 1e6, N / sum(ms) * 1e3))
 import ctypes
 from system_identification_amd import engine as _E
 cfg = (ctypes.c_int32 * 4)()
