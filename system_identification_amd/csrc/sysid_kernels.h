@@ -1845,12 +1845,15 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
       }
     }
   };
-  // Loads are unconditional (a masked load became an exec-masked branch with its own vmcnt(0) wait) at
-  // immediate offsets 16 b from one row address.  Lanes of block 9 whose column is past the row (16 b + kc >=
-  // ldp) read the next row's first columns: what they add lands only in Gram entries past column ldp - 1, which
-  // K3 never writes.  The panel's very last pair is the exception (those reads would run past the panel, and an
-  // odd last sample leaves half the pair's rows unwritten): its units clamp the column into the row and the row
-  // into the pair, and scale missing rows by 0 (the clamped address reads a finite panel value).
+  // Loads are unconditional (a masked load became an exec-masked branch with its own vmcnt(0) wait), agent-scope
+  // (`sc1`: served by L2, never by this CU's L1, whose copy of a line may predate the K1 store that published
+  // it), at immediate offsets 16 b from one row address.  Lanes of the last block whose column is past the row
+  // (16 b + kc >= ldp) read the row's last column instead: a read into the next row would pull the NEXT pair's
+  // first line in before that pair is written (measured: a NaN-filled panel came back as a NaN Gram with plain /
+  // nt loads over-reading), and what those lanes add lands only in Gram entries past column ldp - 1 anyway, which
+  // K3 never writes.  The panel's last pair and an odd last sample run the clamped, zero-scaled loads.
+  auto ld_sc1 = [](const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const int clast = 16 * (NB - 1) + kc < ldp ? 16 * (NB - 1) : (int)ldp - 1 - kc;  // the last block's column
   auto pair_base = [&](int64_t p, const double*& base, int& nrows) {
     const int64_t s0 = f0 + 2 * p;
     nrows = (f1 - s0 >= 2 ? 2 : 1) * NVC;
@@ -1874,7 +1877,8 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
   auto issue = [&](const double* base, int k, double (&f)[NB]) {
     const double* rowp = base + (int64_t)(4 * k) * ldp;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) f[b] = __builtin_nontemporal_load(rowp + 16 * b);
+    for (int b = 0; b < NB - 1; ++b) f[b] = ld_sc1(rowp + 16 * b);
+    f[NB - 1] = ld_sc1(rowp + clast);
   };
   auto issue_edge = [&](const double* base, int nrows, int k, double (&f)[NB]) {
     const int r = 4 * k + kr;
@@ -1884,7 +1888,7 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int c = 16 * b + kc < ldp ? 16 * b : (int)ldp - 1 - kc;
-      f[b] = __builtin_nontemporal_load(rowp + c) * rs;
+      f[b] = ld_sc1(rowp + c) * rs;
     }
   };
   auto mma = [&](const double (&f)[NB]) {
