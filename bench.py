@@ -198,8 +198,7 @@ def main():
     flags = EMIT_ALL
     tflags = EMIT_ALL | GRAM_PRECISION[args.precision] | GRAM_ROWS[args.rows]
     rows_used = args.rows if args.rows != "auto" else eng.gram_rows(args.precision)
-    # one explicit (non-null) stream for every launch, the exchange and the step events: the null stream's handle
-    # is 0, which the C ABI reads as "the engine's own stream" (events on the null stream would not see the work)
+    # one explicit (non-null) stream for every launch, the exchange and the step events
     stream = torch.cuda.Stream(device=local)
     torch.cuda.set_stream(stream)
 

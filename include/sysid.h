@@ -25,7 +25,10 @@
  *     a message.  Python maps E_INVALID/E_MODEL/E_CONTACT to ValueError, E_DEVICE/E_NOMEM to RuntimeError.
  *   - A handle is bound to one device and owns one HIP stream.  The host-buffer entry points (sysid_build,
  *     sysid_build_full, sysid_tau_error) use buffers owned by the handle: they are synchronous and not
- *     re-entrant (one thread at a time per handle).  The device entry points keep every piece of per-launch
+ *     re-entrant (one thread at a time per handle).  The device entry points enqueue on the stream they are
+ *     given, NULL being the device's null stream (the engine's own stream is not ordered with the caller's
+ *     writes of the buffers; round 3's illegal access and round 4's NaN panel were launches left on it while
+ *     PyTorch freed or refilled the buffers on the default stream).  They keep every piece of per-launch
  *     state in the caller's workspace (K1's sample counters, one per XCD shard of the samples, are its first
  *     1 KiB, zeroed on the launch stream before each launch): launches of one handle on different streams with
  *     different workspaces may run concurrently, and an aborted launch leaves nothing behind for the next one.
@@ -130,7 +133,8 @@ size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags);
  *   d_in     : (nq + 2nv + nj + n_contact) x ld channel block [q; dq; ddq; tau; cnt], float64
  *   d_panel  : (N·nv) x ld_panel panel (see layout above); always written
  *   d_gram   : (W+1) x (W+1) Gram, written when flags & SYSID_EMIT_GRAM
- *   stream   : hipStream_t, or NULL for the engine's own stream.
+ *   stream   : hipStream_t; NULL is the device's null stream (ordered with PyTorch's default stream), never
+ *              the engine's own stream, which is not ordered with the caller's work on the buffers.
  * Inputs are not validated on the device (see sysid_check_contacts). */
 int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
                            double* d_panel, int64_t ld_panel, double* d_gram,

@@ -1108,7 +1108,7 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
   if (reinterpret_cast<uintptr_t>(d_panel) & 15)
     return set_err(e, SYSID_E_INVALID, "d_panel must be 16-byte aligned (the panel is written with 16-byte stores)");
   HIP_TRY(e, hipSetDevice(e->device));
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     if (flags & SYSID_EMIT_GRAM)
       HIP_TRY(e, hipMemsetAsync(d_gram, 0, (size_t)e->ncol * e->ncol * sizeof(double), st));
@@ -1128,7 +1128,7 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
   if (N < 0 || ld < N || (N > 0 && !d_in) || !d_gram)
     return set_err(e, SYSID_E_INVALID, "bad arguments (N=%lld ld=%lld)", (long long)N, (long long)ld);
   HIP_TRY(e, hipSetDevice(e->device));
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     HIP_TRY(e, hipMemsetAsync(d_gram, 0, (size_t)e->ncol * e->ncol * sizeof(double), st));
     return SYSID_OK;
@@ -1148,7 +1148,7 @@ int32_t sysid_tau_error_device(sysid_engine* e, const double* d_panel, int64_t l
       (reinterpret_cast<uintptr_t>(d_panel) & 15))
     return set_err(e, SYSID_E_INVALID, "bad arguments");
   HIP_TRY(e, hipSetDevice(e->device));
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     HIP_TRY(e, hipMemsetAsync(d_err_sq, 0, (size_t)e->nv * sizeof(double), st));
     return SYSID_OK;
@@ -1262,6 +1262,7 @@ int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_
                           int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, int32_t iters, double* ms) {
   if (!e || !ms || iters <= 0 || N <= 0) return set_err(e, SYSID_E_INVALID, "bad arguments");
   HIP_TRY(e, hipSetDevice(e->device));
+  HIP_TRY(e, hipDeviceSynchronize());  // the caller's buffers, written on any stream, are complete
   double acc[3] = {0, 0, 0};
   int rc = SYSID_OK;
   if (d_panel == nullptr) {

@@ -1780,7 +1780,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 // pairs w, w + 4, ... of that range (k1_body, FUSED = 1), writing the stacked panel to HBM as the standalone K1
 // does.  A K1 wave publishes, in LDS, how many of its steps have completed (their stores acknowledged by L2:
 // s_waitcnt vmcnt(0)); the Gram waves walk the workgroup's pairs in order and read each pair's 36 rows back from
-// L2 as MFMA fragments (nontemporal loads, served by L2, never by a possibly stale L1 line), accumulating their
+// L2 as MFMA fragments (nontemporal loads), accumulating their
 // tiles in registers: no LDS staging, no barrier, and no re-read of the panel from HBM.  Each Gram wave owns a
 // fixed set of the Gram's 55 upper 16x16 tiles (k12_role: block columns paired high with low, 14/14/14/13
 // tiles) and writes them to its workgroup's slab once at the end; K3 sums the slabs as after K2.
@@ -1845,14 +1845,13 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
       }
     }
   };
-  // Loads are unconditional (a masked load became an exec-masked branch with its own vmcnt(0) wait), agent-scope
-  // (`sc1`: served by L2, never by this CU's L1, whose copy of a line may predate the K1 store that published
-  // it), at immediate offsets 16 b from one row address.  Lanes of the last block whose column is past the row
-  // (16 b + kc >= ldp) read the row's last column instead: a read into the next row would pull the NEXT pair's
-  // first line in before that pair is written (measured: a NaN-filled panel came back as a NaN Gram with plain /
-  // nt loads over-reading), and what those lanes add lands only in Gram entries past column ldp - 1 anyway, which
-  // K3 never writes.  The panel's last pair and an odd last sample run the clamped, zero-scaled loads.
-  auto ld_sc1 = [](const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  // Loads are unconditional (a masked load became an exec-masked branch with its own vmcnt(0) wait), at
+  // immediate offsets 16 b from one row address.  Lanes of the last block whose column is past the row
+  // (16 b + kc >= ldp) read the row's last column instead of the next row's first ones: what they add lands only
+  // in Gram entries past column ldp - 1, which K3 never writes, and no load leaves the pair's rows.  The K1 stores
+  // and these loads run on one CU (one L1, one L2): the workgroup-scope acquire of the ready count orders them.
+  // The panel's last pair and an odd last sample run the clamped, zero-scaled loads.
+  auto ld_nt = [](const double* p) { return __builtin_nontemporal_load(p); };
   const int clast = 16 * (NB - 1) + kc < ldp ? 16 * (NB - 1) : (int)ldp - 1 - kc;  // the last block's column
   auto pair_base = [&](int64_t p, const double*& base, int& nrows) {
     const int64_t s0 = f0 + 2 * p;
@@ -1877,8 +1876,8 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
   auto issue = [&](const double* base, int k, double (&f)[NB]) {
     const double* rowp = base + (int64_t)(4 * k) * ldp;
 #pragma unroll
-    for (int b = 0; b < NB - 1; ++b) f[b] = ld_sc1(rowp + 16 * b);
-    f[NB - 1] = ld_sc1(rowp + clast);
+    for (int b = 0; b < NB - 1; ++b) f[b] = ld_nt(rowp + 16 * b);
+    f[NB - 1] = ld_nt(rowp + clast);
   };
   auto issue_edge = [&](const double* base, int nrows, int k, double (&f)[NB]) {
     const int r = 4 * k + kr;
@@ -1888,7 +1887,7 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int c = 16 * b + kc < ldp ? 16 * b : (int)ldp - 1 - kc;
-      f[b] = ld_sc1(rowp + c) * rs;
+      f[b] = ld_nt(rowp + c) * rs;
     }
   };
   auto mma = [&](const double (&f)[NB]) {

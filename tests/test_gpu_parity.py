@@ -181,6 +181,44 @@ def test_device_api_views_and_determinism():
     assert torch.equal(g1, bufs["gram"])
 
 
+@pytest.mark.parametrize("robot", ["spot", "g1_29dof"])
+def test_null_stream_is_ordered_with_the_default_stream(robot):
+    """stream=None / NULL is the device's null stream: a launch is ordered after PyTorch's default-stream writes
+    of its buffers and before the reads and frees that follow.  (Round 3's illegal access and round 4's NaN panel:
+    NULL used to select the engine's own non-blocking stream, which raced a 400 MB default-stream fill_.)"""
+    import torch
+    model = load_robot(robot)
+    e = eng(robot)
+    N = 20000
+    d = generate(model, N, config_index=8)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_device(N, EMIT_ALL)
+    e.build_device(din, N, EMIT_ALL, bufs)
+    torch.cuda.synchronize()
+    P0, G0 = bufs["panel"][: N * e.nv].clone(), bufs["gram"].clone()
+    gb = e.alloc_gram_device(N)
+    e.build_gram_device(din, N, gb)
+    torch.cuda.synchronize()
+    H0 = gb["gram"].clone()
+    for _ in range(2):
+        bufs["panel"].fill_(float("nan"))
+        bufs["ws"].fill_(255)
+        bufs["gram"].fill_(float("nan"))
+        e.build_device(din, N, EMIT_ALL, bufs)  # no synchronize: stream order alone
+        assert torch.equal(bufs["panel"][: N * e.nv], P0) and torch.equal(bufs["gram"], G0)
+        gb["ws"].fill_(255)
+        gb["gram"].fill_(float("nan"))
+        e.build_gram_device(din, N, gb)
+        assert torch.equal(gb["gram"], H0)
+    # a buffer freed right after the launch (the caching allocator reuses it on the same stream)
+    tmp = e.alloc_device(N, EMIT_ALL)
+    e.build_device(din, N, EMIT_ALL, tmp)
+    del tmp
+    junk = torch.full((N * e.nv, e.panel_ld), float("nan"), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    del junk
+
+
 @pytest.mark.parametrize("robot,N", [("spot", 100000), ("g1_29dof", 20000)])
 def test_full_size_properties(robot, N):
     import torch
