@@ -377,11 +377,16 @@ def main():
     n_time = N
     fused = eng.fused(tflags & ~0x7 if args.gram_only else flags)  # K12: K1 + Gram in one launch (ms[1] = 0)
     ms = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-    ms_unfused = None
+    ms_unfused, ms_fused = None, None
     if fused:  # the same stages with fusion off, for the record (K1 -> K2 -> K3 as three launches)
         eng.set_fusion(False)
         ms_unfused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
         eng.set_fusion(True)
+    else:  # fusion off (the default: measured slower), the fused kernel's time for the record where it exists
+        eng.set_fusion(True)
+        if eng.fused(tflags & ~0x7 if args.gram_only else flags):
+            ms_fused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
+        eng.set_fusion(False)
     nv, W = model.nv, eng.w
     in_b = (model.nq + 2 * nv + model.nj + model.n_ee) * 8
     esize = {"f64": 8, "f32": 4, "bf16": 2}[args.precision] if args.gram_only else 8
@@ -475,6 +480,9 @@ def main():
         "kernel_ms_unfused": None if ms_unfused is None else {
             "K1_regressor_panel": round(ms_unfused[0], 5), "K2_gram_syrk": round(ms_unfused[1], 5),
             "K3_gram_reduce": round(ms_unfused[2], 5), "note": "the same step with fusion off (sysid_set_fusion)"},
+        "kernel_ms_fused": None if ms_fused is None else {
+            "K12_fused_panel_gram": round(ms_fused[0], 5), "K3_gram_reduce": round(ms_fused[2], 5),
+            "note": "the same step with the fused K1 + Gram kernel (sysid_set_fusion(1), off by default: slower)"},
         "K1_GBps": None if fused else round(k1_gbs, 1), "K2_TFps": None if fused else round(k2_tfs, 3),
         "roofline": roof,
         "step_roofline": {"hbm_bytes": step_bytes, "hbm_floor_ms": round(hbm_floor, 5),

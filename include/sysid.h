@@ -30,8 +30,9 @@
  *     writes of the buffers; round 3's illegal access and round 4's NaN panel were launches left on it while
  *     PyTorch freed or refilled the buffers on the default stream).  They keep every piece of per-launch
  *     state in the caller's workspace (K1's sample counters, one per XCD shard of the samples, are its first
- *     1 KiB, zeroed on the launch stream before each launch): launches of one handle on different streams with
- *     different workspaces may run concurrently, and an aborted launch leaves nothing behind for the next one.
+ *     1 KiB, zeroed by a kernel on the launch stream before each launch; no hipMemsetAsync, whose graph node a
+ *     replay did not order after the stream's earlier writes): launches of one handle on different streams
+ *     with different workspaces may run concurrently, and an aborted launch leaves nothing behind.
  *   - Every argument check of an entry point happens before its first enqueue: an error return means that
  *     nothing was enqueued (also under graph capture).
  *
@@ -242,9 +243,11 @@ int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
  * Gram-only (sysid_build_gram_device, f64, projector rows): the rows go through per-wave rings of three sample
  * pairs in the workspace (~140 MB, they stay on-die) instead of chunk panels; SYSID_GRAM_NULLSPACE keeps the
  * unfused nullspace-row path.  Same outputs and contracts (the Gram differs from the unfused path's only in
- * summation order, ~1e-16 relative).  On by default where supported (environment SYSID_FUSE=0 turns it off at
- * engine creation); sysid_set_fusion switches it per engine; sysid_fused tells whether `flags` run fused (with a
- * stacked-output flag: sysid_build_device; without: sysid_build_gram_device). */
+ * summation order, ~1e-16 relative).  Off by default: beside the Gram waves the K1 waves run at half their
+ * standalone occupancy (both are register-bound at two waves per SIMD), so the fused launch measured slower than
+ * K1 -> K2 -> K3 (Spot 20k: 0.445 vs 0.37 ms).  sysid_set_fusion (or SYSID_FUSE=1 at engine creation) turns
+ * it on; sysid_fused tells whether `flags` run fused (with a stacked-output flag: sysid_build_device; without:
+ * sysid_build_gram_device). */
 int32_t sysid_set_fusion(sysid_engine* e, int32_t on);
 int32_t sysid_fused(const sysid_engine* e, uint32_t flags);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */

@@ -134,7 +134,7 @@ struct sysid_engine {
   } k2d[3];
   // K12: the fused K1 + Gram kernel of the full-output f64 path (quadruped K1, 10 tile columns): usable (k12_ok),
   // enabled (fuse: sysid_set_fusion), its dynamic LDS and the K3 tile table of its slab slots
-  int k12_ok = 0, fuse = 1;
+  int k12_ok = 0, fuse = 0;  // the fused kernel is opt-in: measured slower
   size_t k12_lds = 0;
   int2* d_k12_tiles = nullptr;
   // host-API buffers (grow-only)
@@ -252,12 +252,20 @@ size_t prec_bytes(int prec) { return prec == 0 ? 8 : prec == 1 ? 4 : 2; }
 // Gram arithmetic selected by the flags: 0 = f64 (parity), 1 = f32 MFMA, 2 = bf16 MFMA (error reported).
 int gram_prec(uint32_t flags) { return (flags & SYSID_GRAM_BF16) ? 2 : (flags & SYSID_GRAM_F32) ? 1 : 0; }
 
+// zero `bytes` (a multiple of 8) on `st` with a kernel (see k0_zero_u64: graph-safe, unlike hipMemsetAsync)
+hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
+  const int64_t n = (int64_t)(bytes / sizeof(unsigned long long));
+  const unsigned g = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 255) / 256));
+  hipLaunchKernelGGL(k0_zero_u64, dim3(g), dim3(256), 0, st, static_cast<unsigned long long*>(p), n);
+  return hipGetLastError();
+}
+
 // cmp: the Gram-only nullspace mode (rcount: its per-sample row counts).
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
               unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0, int cmp = 0,
               int* rcount = nullptr) {
   K1Params kp = e->kp;
-  HIP_TRY(e, hipMemsetAsync(work, 0, WORK_BYTES, st));
+  HIP_TRY(e, zero_async(work, WORK_BYTES, st));
   if (full) {
     kp.full = 1;
     kp.in_rows = e->in_lds;
@@ -1111,7 +1119,7 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     if (flags & SYSID_EMIT_GRAM)
-      HIP_TRY(e, hipMemsetAsync(d_gram, 0, (size_t)e->ncol * e->ncol * sizeof(double), st));
+      HIP_TRY(e, zero_async(d_gram, (size_t)e->ncol * e->ncol * sizeof(double), st));
     return SYSID_OK;
   }
   return launch_stages(e, d_in, N, ld, flags, d_panel, ld_panel, d_gram, d_ws, ws_bytes, st, nullptr);
@@ -1130,7 +1138,7 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
   HIP_TRY(e, hipSetDevice(e->device));
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
-    HIP_TRY(e, hipMemsetAsync(d_gram, 0, (size_t)e->ncol * e->ncol * sizeof(double), st));
+    HIP_TRY(e, zero_async(d_gram, (size_t)e->ncol * e->ncol * sizeof(double), st));
     return SYSID_OK;
   }
   return launch_gram_chunked(e, d_in, N, ld, flags, d_gram, d_ws, ws_bytes, st);
@@ -1150,7 +1158,7 @@ int32_t sysid_tau_error_device(sysid_engine* e, const double* d_panel, int64_t l
   HIP_TRY(e, hipSetDevice(e->device));
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
-    HIP_TRY(e, hipMemsetAsync(d_err_sq, 0, (size_t)e->nv * sizeof(double), st));
+    HIP_TRY(e, zero_async(d_err_sq, (size_t)e->nv * sizeof(double), st));
     return SYSID_OK;
   }
   return launch_k4(e, d_panel, ld_panel, N, d_phi, d_err_sq, d_ws, ws_bytes, st);

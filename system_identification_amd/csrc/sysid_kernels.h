@@ -2007,6 +2007,14 @@ __device__ __forceinline__ int k1s_wave_incl(int v, int lane) {  // inclusive sc
 }
 
 #ifndef SYSID_TEMPLATE_TU  // the non-template kernels live in sysid_engine.hip's translation unit only
+// Zeroing on the device entry points' streams is done by kernels, never hipMemsetAsync: captured into a HIP graph,
+// a memset became a node that a replay did not order after the default-stream writes just before it (measured:
+// a 0xFF-filled workspace replayed into claim counters still at 0xFF..., so K1 claimed no samples and the Gram
+// came back NaN or empty; tools/dbg_ns_graph.py, profiles/r04_dbg).  Kernel nodes are ordered.
+__global__ void __launch_bounds__(256) k0_zero_u64(unsigned long long* __restrict__ p, int64_t n) {
+  for (int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) p[x] = 0ull;
+}
+
 __global__ void __launch_bounds__(256)
 k1s_seg_sums(const int* __restrict__ rcount, int n, int* __restrict__ rseg) {
   __shared__ int wsum[4];

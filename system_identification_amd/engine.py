@@ -383,7 +383,7 @@ class Engine:
         self._check(self.lib.sysid_set_gram_chunk_bytes(self._h, int(nbytes)))
 
     def set_fusion(self, on: bool) -> None:
-        """Fused K1 + Gram for the full-output f64 Gram (sysid_set_fusion; on by default where supported)."""
+        """Fused K1 + Gram for the quadrupeds' f64 Grams (sysid_set_fusion; off by default: measured slower)."""
         self._check(self.lib.sysid_set_fusion(self._h, 1 if on else 0))
 
     def fused(self, flags: int = EMIT_ALL) -> bool:
