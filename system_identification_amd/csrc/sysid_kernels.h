@@ -1325,7 +1325,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     // the step's rows: the stacked panel's, or (fused Gram-only) the ring slot of this step
     OutT* const obase = FUSED == 2 ? panel + (int64_t)((steps_done % (k12_ring > 0 ? k12_ring : 1)) * SPW) * nv * ldp
                                    : panel + s * nv * ldp;
-    OutT* out = obase + (int64_t)half * nv * ldp;
+    OutT* out = FUSED ? obase + (int64_t)half * nv * ldp : panel + ((s + half) * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
     auto block_row = [&](int r, const double* F, const int* dof, int cl, double* y) {
       const double* h = h1_in_p ? Ps + r * nv + kp.ff0 : H1 + 6 * r;
@@ -1412,7 +1412,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       // 2x, plus dg for the second group.  The row start of the wave's first sample is wave-uniform (scalar
       // registers); the second sample's rows and the column go into a 32-bit lane byte offset, so each store is
       // a scalar-base + lane-offset store with no 64-bit address math.
-      char* ybase = reinterpret_cast<char*>(obase);
+      char* ybase = reinterpret_cast<char*>(FUSED ? obase : panel + (s * NVC) * ldp);
       const uint32_t yhoff = (uint32_t)(half * NVC * (int)ldp * (int)sizeof(OutT));
       const int dg = rh * (int)ldp - kp.wy;
       // Rows in pairs with two explicit H1 / P register sets (no copies between them): row rho + 1's LDS reads
