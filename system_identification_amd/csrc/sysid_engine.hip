@@ -152,6 +152,8 @@ struct sysid_engine {
   double* h_stage = nullptr;  // host API: page-locked staging of the input block (grow-only)
   size_t h_stage_cap = 0;
   HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
+  hipStream_t copy_stream = nullptr;     // host API: the staged input chunks' DMA (created on first use)
+  std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
 
@@ -492,8 +494,11 @@ int gram_nullspace(const sysid_engine* e, uint32_t flags) {
   return want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
 }
 
+// staged (host entry point): chunks of `staged_chunk` samples, chunk c's K1 waiting on event ready[c] (its inputs'
+// DMA on the copy stream); 0 / nullptr: the workspace's chunk size, inputs already on the device.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
-                        void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr) {
+                        void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
+                        int64_t staged_chunk = 0, const hipEvent_t* ready = nullptr) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
@@ -512,6 +517,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
       return SYSID_OK;
     };
     int rc;
+    if (ready) HIP_TRY(e, hipStreamWaitEvent(st, ready[(N - 1) / staged_chunk], 0));  // every chunk's DMA
     if ((rc = mark())) return rc;
     if ((rc = launch_k12(e, d_in, N, ld, ring, e->ldp, slab, st, 1))) return rc;
     while (ev && k + 1 < ev->size())
@@ -536,8 +542,10 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     if (ev && k < ev->size()) HIP_TRY(e, hipEventRecord((*ev)[k++], st));
     return SYSID_OK;
   };
-  for (int64_t c0 = 0; c0 < N; c0 += C) {
-    const int64_t n = std::min(C, N - c0);
+  const int64_t step = staged_chunk > 0 && staged_chunk < C ? staged_chunk : C;
+  for (int64_t c0 = 0; c0 < N; c0 += step) {
+    const int64_t n = std::min(step, N - c0);
+    if (ready) HIP_TRY(e, hipStreamWaitEvent(st, ready[(c0 + n - 1) / staged_chunk], 0));  // this chunk's inputs
     if ((rc = mark())) return rc;
     if (cmp) {
       if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount)))
@@ -604,9 +612,12 @@ int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemc
 // largest part of the Gram-only e2e step).  Here host threads pack the channels into the engine's page-locked
 // staging block chunk by chunk (samples [c0, c1) of every channel) and each finished chunk leaves as one 2-D DMA
 // while the threads pack the next, so the copy engine runs at PCIe rate beside the packing.  Returns with every
-// chunk enqueued on `st` (the staging block is reused by the next call only after that call's stream sync).
+// chunk enqueued on the engine's copy stream, chunk c followed by event stage_ev[c]; *chunk = samples per chunk
+// (the last may be shorter).  The caller makes its launch stream wait on the events (the Gram-only path: chunk c's
+// K1 on event c, so the DMA of chunk c + 1 runs beside it) and synchronises that stream before the next call
+// reuses the staging block.
 int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, int nsrc, int64_t N, int64_t ld,
-                 double* d_dst, hipStream_t st) {
+                 double* d_dst, int64_t* chunk) {
   const size_t need = (size_t)e->in_rows * N * sizeof(double);
   if (need > e->h_stage_cap) {
     if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -627,6 +638,14 @@ int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, i
   const int T = e->pool->size();
   const int64_t CH = std::max<int64_t>(4096, (N + 7) / 8);  // samples per chunk
   const int nch = (int)((N + CH - 1) / CH);
+  if (!e->copy_stream) HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+  while ((int)e->stage_ev.size() < nch) {
+    hipEvent_t x;
+    HIP_TRY(e, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    e->stage_ev.push_back(x);
+  }
+  *chunk = CH;
+  const hipStream_t cs = e->copy_stream;
   std::vector<std::atomic<int>> done(nch);
   for (auto& d : done) d.store(0);
   double* hs = e->h_stage;
@@ -641,8 +660,9 @@ int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, i
   for (int c = 0; c < nch; ++c) {
     while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
     const int64_t c0 = c * CH, n = std::min(CH, N - c0);
-    if (rc == SYSID_OK && hipMemcpy2DAsync(d_dst + c0, (size_t)N * sizeof(double), hs + c0, (size_t)N * sizeof(double),
-                                           (size_t)n * sizeof(double), R, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (rc == SYSID_OK && (hipMemcpy2DAsync(d_dst + c0, (size_t)N * sizeof(double), hs + c0, (size_t)N * sizeof(double),
+                                            (size_t)n * sizeof(double), R, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                           hipEventRecord(e->stage_ev[c], cs) != hipSuccess))
       rc = set_err(e, SYSID_E_DEVICE, "input copy failed");
   }
   e->pool->wait();
@@ -1059,6 +1079,8 @@ void sysid_destroy(sysid_engine* e) {
     if (p) (void)hipFree(p);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   delete e->pool;
+  for (hipEvent_t x : e->stage_ev) (void)hipEventDestroy(x);
+  if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1350,13 +1372,22 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   if ((rc = grow(e, &e->d_ws, &e->ws_cap, wsb ? wsb : 256))) return rc;
   hipStream_t st = e->stream;
   std::vector<void*> reg;
-  auto fail = [&](int code) { (void)hipStreamSynchronize(st); host_unregister(e, reg); return code; };
+  auto fail = [&](int code) {
+    (void)hipStreamSynchronize(st);
+    if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
+    host_unregister(e, reg);
+    return code;
+  };
   // inputs: channel c of the caller's arrays -> row c of the device block: staged through page-locked memory by
   // host threads for blocks of 1 MiB and more (stage_inputs), else one copy per array
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
   const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
-  if (staged && (rc = stage_inputs(e, srcs, nrows, 5, N, ld, e->d_in, st)) != SYSID_OK) return fail(rc);
+  int64_t sch = 0;  // staged: samples per DMA chunk (stage_ev[c] marks chunk c on the copy stream)
+  if (staged && (rc = stage_inputs(e, srcs, nrows, 5, N, ld, e->d_in, &sch)) != SYSID_OK) return fail(rc);
+  // the stacked-output path reads every sample in one launch: all chunks first
+  if (staged && !gram_only && hipStreamWaitEvent(st, e->stage_ev[(N - 1) / sch], 0) != hipSuccess)
+    return fail(set_err(e, SYSID_E_DEVICE, "stream wait failed"));
   int64_t r0 = 0;
   for (int k = 0; k < 5 && !staged; ++k) {
     if (nrows[k] > 0) {
@@ -1371,7 +1402,8 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     r0 += nrows[k];
   }
-  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st)
+  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, sch,
+                                       staged ? e->stage_ev.data() : nullptr)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
   if (rc != SYSID_OK) return fail(rc);
   if (panel_out) {
