@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -1343,12 +1344,19 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   if (N < 0 || ld < N) return set_err(e, SYSID_E_INVALID, "bad N/ld (%lld/%lld)", (long long)N, (long long)ld);
   if (N > 0 && (!q || !dq || !ddq || (!tau && e->nj) || (!cnt && e->nc)))
     return set_err(e, SYSID_E_INVALID, "null input buffer");
+  // SYSID_TRACE_HOST=1: host-clock phase times of this call on stderr (diagnostics of the e2e number)
+  static const bool trace = std::getenv("SYSID_TRACE_HOST") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = clk::now();
+  double tph[4] = {0, 0, 0, 0};
+  auto ms_since = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   if (N > 0 && e->nc) {
     const int rc = sysid_check_contacts(e, cnt, N, ld, nullptr);
     if (rc != SYSID_OK) return rc;
   }
   const bool want_gram = (flags & SYSID_EMIT_GRAM) && (gram || Atb || btb);
   if (want_gram) flags |= SYSID_EMIT_GRAM; else flags &= ~SYSID_EMIT_GRAM;
+  tph[0] = ms_since(t0);  // contact check
   HIP_TRY(e, hipSetDevice(e->device));
   if (N == 0) {
     const size_t W = (size_t)e->w;
@@ -1388,6 +1396,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   // the stacked-output path reads every sample in one launch: all chunks first
   if (staged && !gram_only && hipStreamWaitEvent(st, e->stage_ev[(N - 1) / sch], 0) != hipSuccess)
     return fail(set_err(e, SYSID_E_DEVICE, "stream wait failed"));
+  tph[1] = ms_since(t0);  // + buffers, packing, every input DMA enqueued
   int64_t r0 = 0;
   for (int k = 0; k < 5 && !staged; ++k) {
     if (nrows[k] > 0) {
@@ -1437,8 +1446,13 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     if (btb && hipMemcpyAsync(btb, e->d_gram + W * e->ncol + W, sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
       return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
   }
+  tph[2] = ms_since(t0);  // + kernels and output copies enqueued
   const hipError_t sst = hipStreamSynchronize(st);
   host_unregister(e, reg);
+  tph[3] = ms_since(t0);  // + synchronised
+  if (trace)
+    std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staged+DMA enqueued %.3f, launched %.3f, "
+                 "done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], tph[2], tph[3]);
   if (sst != hipSuccess) return set_err(e, SYSID_E_DEVICE, "stream sync failed: %s", hipGetErrorString(sst));
   return SYSID_OK;
 }

@@ -311,7 +311,9 @@ def test_gram_only_chunked(robot, N):
     e.build_gram_device(din, N, bufs)
     torch.cuda.synchronize()
     G1 = bufs["gram"].clone()
-    assert np.array_equal(G1[:e.w, :e.w].cpu().numpy(), only["gram"])
+    # the host path chunks along its staged input DMA (each chunk's K1 starts when its inputs land): the same
+    # Gram to rounding, summed in a different chunk order
+    assert rel(G1[:e.w, :e.w].cpu().numpy(), only["gram"]) < 1e-12
     e.build_gram_device(din, N, bufs)
     torch.cuda.synchronize()
     assert torch.equal(G1, bufs["gram"])
