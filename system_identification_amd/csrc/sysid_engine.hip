@@ -17,6 +17,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -495,11 +496,12 @@ int gram_nullspace(const sysid_engine* e, uint32_t flags) {
   return want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
 }
 
-// staged (host entry point): chunks of `staged_chunk` samples, chunk c's K1 waiting on event ready[c] (its inputs'
-// DMA on the copy stream); 0 / nullptr: the workspace's chunk size, inputs already on the device.
+// staged (host entry point): chunks of at most `staged_chunk` samples, and (*stage_upto)(n) before the K1 of a
+// chunk ending at sample n (it orders `st` after the DMA of the inputs [0, n)); 0 / nullptr: the workspace's chunk
+// size, inputs already on the device.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
-                        int64_t staged_chunk = 0, const hipEvent_t* ready = nullptr) {
+                        int64_t staged_chunk = 0, const std::function<int(int64_t)>* stage_upto = nullptr) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
@@ -518,7 +520,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
       return SYSID_OK;
     };
     int rc;
-    if (ready) HIP_TRY(e, hipStreamWaitEvent(st, ready[(N - 1) / staged_chunk], 0));  // every chunk's DMA
+    if (stage_upto && (rc = (*stage_upto)(N))) return rc;  // every chunk's DMA
     if ((rc = mark())) return rc;
     if ((rc = launch_k12(e, d_in, N, ld, ring, e->ldp, slab, st, 1))) return rc;
     while (ev && k + 1 < ev->size())
@@ -546,7 +548,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   const int64_t step = staged_chunk > 0 && staged_chunk < C ? staged_chunk : C;
   for (int64_t c0 = 0; c0 < N; c0 += step) {
     const int64_t n = std::min(step, N - c0);
-    if (ready) HIP_TRY(e, hipStreamWaitEvent(st, ready[(c0 + n - 1) / staged_chunk], 0));  // this chunk's inputs
+    if (stage_upto && (rc = (*stage_upto)(c0 + n))) return rc;  // this chunk's inputs
     if ((rc = mark())) return rc;
     if (cmp) {
       if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount)))
@@ -608,67 +610,88 @@ int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemc
   return SYSID_OK;
 }
 
-// Host entry points: the caller's channel arrays (pageable numpy memory) -> the device input block, at DMA speed.
-// A pageable copy runs at the speed of the runtime's single staging memcpy (Spot 20k: 11.4 MB at ~17 GB/s, the
-// largest part of the Gram-only e2e step).  Here host threads pack the channels into the engine's page-locked
-// staging block chunk by chunk (samples [c0, c1) of every channel) and each finished chunk leaves as one 2-D DMA
-// while the threads pack the next, so the copy engine runs at PCIe rate beside the packing.  Returns with every
-// chunk enqueued on the engine's copy stream, chunk c followed by event stage_ev[c]; *chunk = samples per chunk
-// (the last may be shorter).  The caller makes its launch stream wait on the events (the Gram-only path: chunk c's
-// K1 on event c, so the DMA of chunk c + 1 runs beside it) and synchronises that stream before the next call
-// reuses the staging block.
-int stage_inputs(sysid_engine* e, const double* const* srcs, const int* nrows, int nsrc, int64_t N, int64_t ld,
-                 double* d_dst, int64_t* chunk) {
-  const size_t need = (size_t)e->in_rows * N * sizeof(double);
-  if (need > e->h_stage_cap) {
-    if (e->h_stage) (void)hipHostFree(e->h_stage);
-    e->h_stage = nullptr;
-    e->h_stage_cap = 0;
-    HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
-    e->h_stage_cap = need;
-  }
-  std::vector<const double*> row_src;  // channel row r of the block <- its source row
-  for (int k = 0; k < nsrc; ++k)
-    for (int r = 0; r < nrows[k]; ++r) row_src.push_back(srcs[k] + (int64_t)r * ld);
-  const int R = (int)row_src.size();
-  if (!e->pool) {
-    int T = 8;  // the GPU box grants a job 16 host threads (OMP_NUM_THREADS): half of them pack
-    if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
-    e->pool = new HostPool(T);
-  }
-  const int T = e->pool->size();
-  const int64_t CH = std::max<int64_t>(4096, (N + 7) / 8);  // samples per chunk
-  const int nch = (int)((N + CH - 1) / CH);
-  if (!e->copy_stream) HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
-  while ((int)e->stage_ev.size() < nch) {
-    hipEvent_t x;
-    HIP_TRY(e, hipEventCreateWithFlags(&x, hipEventDisableTiming));
-    e->stage_ev.push_back(x);
-  }
-  *chunk = CH;
-  const hipStream_t cs = e->copy_stream;
-  std::vector<std::atomic<int>> done(nch);
-  for (auto& d : done) d.store(0);
-  double* hs = e->h_stage;
-  e->pool->start([&](int t) {
-    for (int c = 0; c < nch; ++c) {
-      const int64_t c0 = c * CH, n = std::min(CH, N - c0);
-      for (int r = t; r < R; r += T) std::memcpy(hs + (int64_t)r * N + c0, row_src[r] + c0, (size_t)n * sizeof(double));
-      done[c].fetch_add(1, std::memory_order_release);
+// Host entry points: the caller's channel arrays (pageable numpy memory) -> the device input block, pipelined with
+// the kernels.  Host threads (the engine's pool) pack the channels into the engine's page-locked staging block
+// chunk by chunk (samples [c0, c1) of every channel); stage(c) waits until chunk c is packed, sends it as one 2-D
+// DMA on the engine's copy stream and makes the launch stream wait for that DMA only — so the caller enqueues chunk
+// c's kernels right away and they run while chunk c + 1 is packed and copied (the Gram-only path: K1 / K2 per
+// chunk; the stacked-output path stages every chunk before its single K1).  Measured on Spot 20k Gram-only: the
+// pack-everything-first form took 0.19 ms of packing before the first kernel (profiles/r04_g).  The staging block
+// is reused by the next call only after this call's launch-stream synchronise, which follows every DMA.
+class Stager {
+ public:
+  Stager(sysid_engine* e, int64_t N, double* d_dst) : e_(e), N_(N), d_dst_(d_dst) {}
+  ~Stager() { finish(); }
+  int64_t chunk() const { return CH_; }
+  int chunks() const { return nch_; }
+  int begin(const double* const* srcs, const int* nrows, int nsrc, int64_t ld) {
+    sysid_engine* e = e_;
+    const size_t need = (size_t)e->in_rows * N_ * sizeof(double);
+    if (need > e->h_stage_cap) {
+      if (e->h_stage) (void)hipHostFree(e->h_stage);
+      e->h_stage = nullptr;
+      e->h_stage_cap = 0;
+      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
+      e->h_stage_cap = need;
     }
-  });
-  int rc = SYSID_OK;
-  for (int c = 0; c < nch; ++c) {
-    while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
-    const int64_t c0 = c * CH, n = std::min(CH, N - c0);
-    if (rc == SYSID_OK && (hipMemcpy2DAsync(d_dst + c0, (size_t)N * sizeof(double), hs + c0, (size_t)N * sizeof(double),
-                                            (size_t)n * sizeof(double), R, hipMemcpyHostToDevice, cs) != hipSuccess ||
-                           hipEventRecord(e->stage_ev[c], cs) != hipSuccess))
-      rc = set_err(e, SYSID_E_DEVICE, "input copy failed");
+    for (int k = 0; k < nsrc; ++k)
+      for (int r = 0; r < nrows[k]; ++r) row_src_.push_back(srcs[k] + (int64_t)r * ld);
+    if (!e->pool) {
+      int T = 8;  // the GPU box grants a job 16 host threads (OMP_NUM_THREADS): half of them pack
+      if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
+      e->pool = new HostPool(T);
+    }
+    int parts = 4;  // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few
+    if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
+    CH_ = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
+    nch_ = (int)((N_ + CH_ - 1) / CH_);
+    if (!e->copy_stream) HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+    while ((int)e->stage_ev.size() < nch_) {
+      hipEvent_t x;
+      HIP_TRY(e, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      e->stage_ev.push_back(x);
+    }
+    done_.reset(new std::atomic<int>[nch_]);
+    for (int c = 0; c < nch_; ++c) done_[c].store(0);
+    const int T = e->pool->size(), R = (int)row_src_.size();
+    double* hs = e->h_stage;
+    e->pool->start([this, T, R, hs](int t) {
+      for (int c = 0; c < nch_; ++c) {
+        const int64_t c0 = c * CH_, n = std::min(CH_, N_ - c0);
+        for (int r = t; r < R; r += T) std::memcpy(hs + (int64_t)r * N_ + c0, row_src_[r] + c0, (size_t)n * sizeof(double));
+        done_[c].fetch_add(1, std::memory_order_release);
+      }
+    });
+    started_ = true;
+    return SYSID_OK;
   }
-  e->pool->wait();
-  return rc;
-}
+  // chunk c: wait until packed, DMA it, and order `st` after that DMA
+  int stage(int c, hipStream_t st) {
+    sysid_engine* e = e_;
+    const int T = e->pool->size();
+    while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    const int64_t c0 = c * CH_, n = std::min(CH_, N_ - c0);
+    const double* hs = e->h_stage;
+    if (hipMemcpy2DAsync(d_dst_ + c0, (size_t)N_ * sizeof(double), hs + c0, (size_t)N_ * sizeof(double),
+                         (size_t)n * sizeof(double), row_src_.size(), hipMemcpyHostToDevice, e->copy_stream) != hipSuccess ||
+        hipEventRecord(e->stage_ev[c], e->copy_stream) != hipSuccess || hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
+      return set_err(e, SYSID_E_DEVICE, "input copy failed");
+    return SYSID_OK;
+  }
+  void finish() {
+    if (started_) e_->pool->wait();
+    started_ = false;
+  }
+
+ private:
+  sysid_engine* e_;
+  int64_t N_, CH_ = 0;
+  int nch_ = 0;
+  double* d_dst_;
+  std::vector<const double*> row_src_;  // channel row r of the block <- its source row
+  std::unique_ptr<std::atomic<int>[]> done_;
+  bool started_ = false;
+};
 
 int host_unregister(sysid_engine* e, std::vector<void*>& registered) {
   for (void* p : registered) (void)hipHostUnregister(p);
@@ -1391,12 +1414,19 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
   const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
-  int64_t sch = 0;  // staged: samples per DMA chunk (stage_ev[c] marks chunk c on the copy stream)
-  if (staged && (rc = stage_inputs(e, srcs, nrows, 5, N, ld, e->d_in, &sch)) != SYSID_OK) return fail(rc);
+  Stager stager(e, N, e->d_in);
+  int nstaged = 0;  // chunks sent so far
+  const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
+    for (; nstaged < stager.chunks() && (int64_t)nstaged * stager.chunk() < upto; ++nstaged) {
+      const int r = stager.stage(nstaged, st);
+      if (r != SYSID_OK) return r;
+    }
+    return SYSID_OK;
+  };
+  if (staged && (rc = stager.begin(srcs, nrows, 5, ld)) != SYSID_OK) return fail(rc);
   // the stacked-output path reads every sample in one launch: all chunks first
-  if (staged && !gram_only && hipStreamWaitEvent(st, e->stage_ev[(N - 1) / sch], 0) != hipSuccess)
-    return fail(set_err(e, SYSID_E_DEVICE, "stream wait failed"));
-  tph[1] = ms_since(t0);  // + buffers, packing, every input DMA enqueued
+  if (staged && !gram_only && (rc = stage_upto(N)) != SYSID_OK) return fail(rc);
+  tph[1] = ms_since(t0);  // + buffers, packing started (stacked outputs: every chunk's DMA enqueued)
   int64_t r0 = 0;
   for (int k = 0; k < 5 && !staged; ++k) {
     if (nrows[k] > 0) {
@@ -1411,8 +1441,8 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     r0 += nrows[k];
   }
-  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, sch,
-                                       staged ? e->stage_ev.data() : nullptr)
+  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
+                                       staged ? stager.chunk() : 0, staged ? &stage_upto : nullptr)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
   if (rc != SYSID_OK) return fail(rc);
   if (panel_out) {
@@ -1451,7 +1481,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   host_unregister(e, reg);
   tph[3] = ms_since(t0);  // + synchronised
   if (trace)
-    std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staged+DMA enqueued %.3f, launched %.3f, "
+    std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, launched %.3f, "
                  "done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], tph[2], tph[3]);
   if (sst != hipSuccess) return set_err(e, SYSID_E_DEVICE, "stream sync failed: %s", hipGetErrorString(sst));
   return SYSID_OK;
