@@ -155,6 +155,10 @@ struct sysid_engine {
   size_t h_stage_cap = 0;
   HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
   hipStream_t copy_stream = nullptr;     // host API: the staged input chunks' DMA (created on first use)
+  unsigned* d_in_ready = nullptr;        // host API, streamed inputs: per-part flags + error word (K1Params::in_ready)
+  unsigned* h_in_err = nullptr;          // page-locked copy of the error word
+  unsigned in_epoch = 0;                 // the flags' value of the current call
+  int stream_parts = 4;                  // parts per claim shard (SYSID_STREAM_PARTS; 0: no streaming)
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -264,11 +268,23 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Streamed inputs of one K1 launch (K1Params::in_ready): the host entry point's Gram-only path.
+struct K1Stream {
+  const unsigned* ready;
+  int part;
+  unsigned epoch;
+};
+
 // cmp: the Gram-only nullspace mode (rcount: its per-sample row counts).
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
               unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0, int cmp = 0,
-              int* rcount = nullptr) {
+              int* rcount = nullptr, const K1Stream* kst = nullptr) {
   K1Params kp = e->kp;
+  if (kst) {
+    kp.in_ready = kst->ready;
+    kp.in_part = kst->part;
+    kp.in_epoch = kst->epoch;
+  }
   HIP_TRY(e, zero_async(work, WORK_BYTES, st));
   if (full) {
     kp.full = 1;
@@ -501,7 +517,8 @@ int gram_nullspace(const sysid_engine* e, uint32_t flags) {
 // size, inputs already on the device.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
-                        int64_t staged_chunk = 0, const std::function<int(int64_t)>* stage_upto = nullptr) {
+                        int64_t staged_chunk = 0, const std::function<int(int64_t)>* stage_upto = nullptr,
+                        const K1Stream* kst = nullptr) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
@@ -551,13 +568,13 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     if (stage_upto && (rc = (*stage_upto)(c0 + n))) return rc;  // this chunk's inputs
     if ((rc = mark())) return rc;
     if (cmp) {
-      if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount)))
+      if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, kst)))
         return rc;
       const unsigned nseg = (unsigned)((n + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG);
       hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
       hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, rseg, (int)n, e->nv, rowlist, d_rows);
       HIP_TRY(e, hipGetLastError());
-    } else if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec))) {
+    } else if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr, kst))) {
       return rc;
     }
     if ((rc = mark())) return rc;
@@ -683,9 +700,83 @@ class Stager {
     started_ = false;
   }
 
+  // Streamed form (the Gram-only path when it is one chunk: ONE K1 launch over all N whose waves wait per part,
+  // K1Params::in_ready): the device block's row pitch is `ldd` (a multiple of 16 samples), and part p is the
+  // shard-relative samples [p·PL, (p+1)·PL) of every claim shard (k1_shard_begin), so the K1 waves of every XCD
+  // start on part 0 together.  Packed part by part; send_streamed() then sends part p as one 2-D DMA per shard
+  // piece and flags it (in_ready[p] = epoch, written by the copy stream after those DMAs).
+  int begin_streamed(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, int64_t ldd, int parts) {
+    sysid_engine* e = e_;
+    ldd_ = ldd;
+    const size_t need = (size_t)e->in_rows * ldd * sizeof(double);
+    if (need > e->h_stage_cap) {
+      if (e->h_stage) (void)hipHostFree(e->h_stage);
+      e->h_stage = nullptr;
+      e->h_stage_cap = 0;
+      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
+      e->h_stage_cap = need;
+    }
+    for (int k = 0; k < nsrc; ++k)
+      for (int r = 0; r < nrows[k]; ++r) row_src_.push_back(srcs[k] + (int64_t)r * ld);
+    if (!e->pool) {
+      int T = 8;
+      if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
+      e->pool = new HostPool(T);
+    }
+    int64_t maxlen = 0;
+    for (int x = 0; x < K1_SHARDS; ++x) maxlen = std::max(maxlen, k1_shard_begin(N_, x + 1) - k1_shard_begin(N_, x));
+    parts = std::max(1, std::min(parts, K1_STREAM_ERR));
+    CH_ = std::max<int64_t>(16, ((maxlen + parts - 1) / parts + 15) / 16 * 16);  // PL: whole 128-byte lines
+    nch_ = (int)std::max<int64_t>(1, (maxlen + CH_ - 1) / CH_);
+    if (!e->copy_stream) HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+    done_.reset(new std::atomic<int>[nch_]);
+    for (int c = 0; c < nch_; ++c) done_[c].store(0);
+    const int T = e->pool->size(), R = (int)row_src_.size();
+    double* hs = e->h_stage;
+    e->pool->start([this, T, R, hs](int t) {
+      for (int c = 0; c < nch_; ++c) {
+        for (int x = 0; x < K1_SHARDS; ++x) {
+          int64_t c0, n;
+          piece(c, x, &c0, &n);
+          if (n > 0)
+            for (int r = t; r < R; r += T)
+              std::memcpy(hs + (int64_t)r * ldd_ + c0, row_src_[r] + c0, (size_t)n * sizeof(double));
+        }
+        done_[c].fetch_add(1, std::memory_order_release);
+      }
+    });
+    started_ = true;
+    return SYSID_OK;
+  }
+  int send_streamed(unsigned* d_ready, unsigned epoch) {
+    sysid_engine* e = e_;
+    const int T = e->pool->size();
+    const double* hs = e->h_stage;
+    for (int c = 0; c < nch_; ++c) {
+      while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+      for (int x = 0; x < K1_SHARDS; ++x) {
+        int64_t c0, n;
+        piece(c, x, &c0, &n);
+        if (n > 0 && hipMemcpy2DAsync(d_dst_ + c0, (size_t)ldd_ * sizeof(double), hs + c0, (size_t)ldd_ * sizeof(double),
+                                      (size_t)n * sizeof(double), row_src_.size(), hipMemcpyHostToDevice,
+                                      e->copy_stream) != hipSuccess)
+          return set_err(e, SYSID_E_DEVICE, "input copy failed");
+      }
+      if (hipStreamWriteValue32(e->copy_stream, d_ready + c, epoch, 0) != hipSuccess)
+        return set_err(e, SYSID_E_DEVICE, "input flag write failed");
+    }
+    return SYSID_OK;
+  }
+
  private:
+  void piece(int c, int x, int64_t* c0, int64_t* n) const {  // part c of shard x
+    const int64_t b = k1_shard_begin(N_, x), en = k1_shard_begin(N_, x + 1);
+    *c0 = b + c * CH_;
+    *n = std::max<int64_t>(0, std::min(en, *c0 + CH_) - *c0);
+  }
+
   sysid_engine* e_;
-  int64_t N_, CH_ = 0;
+  int64_t N_, CH_ = 0, ldd_ = 0;
   int nch_ = 0;
   double* d_dst_;
   std::vector<const double*> row_src_;  // channel row r of the block <- its source row
@@ -1005,6 +1096,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("SYSID_STREAM_PARTS")) e->stream_parts = std::max(0, std::atoi(v));
   if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   for (int p = 0; p < 3; ++p) {
@@ -1104,6 +1196,8 @@ void sysid_destroy(sysid_engine* e) {
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   delete e->pool;
   for (hipEvent_t x : e->stage_ev) (void)hipEventDestroy(x);
+  if (e->d_in_ready) (void)hipFree(e->d_in_ready);
+  if (e->h_in_err) (void)hipHostFree(e->h_in_err);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -1393,8 +1487,15 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const bool panel_out = ((flags & SYSID_EMIT_Y) && Y_proj) || ((flags & SYSID_EMIT_TAU) && tau_proj) ||
                          ((flags & SYSID_EMIT_FRICTION) && (B_v || B_c) && e->nj);
   const bool gram_only = want_gram && !panel_out;
+  const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
+  // streamed (Gram-only, one chunk, unfused): one K1 launch consumes the inputs as their parts land
+  const int gp = gram_prec(flags);
+  const bool streamed = staged && gram_only && e->stream_parts > 0 && N <= gram_chunk(e, N, gp) &&
+                        !(gp == 0 && !gram_nullspace(e, flags) && e->k12_ok && e->fuse);
+  const int64_t ldd = streamed ? (N + 15) / 16 * 16 : N;  // device row pitch: whole 128-byte lines when streamed
   int rc;
-  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) return rc;
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * ldd * sizeof(double))))
+    return rc;
   if (!gram_only &&
       (rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
     return rc;
@@ -1413,7 +1514,6 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   // host threads for blocks of 1 MiB and more (stage_inputs), else one copy per array
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
-  const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
   Stager stager(e, N, e->d_in);
   int nstaged = 0;  // chunks sent so far
   const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
@@ -1423,7 +1523,20 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     return SYSID_OK;
   };
-  if (staged && (rc = stager.begin(srcs, nrows, 5, ld)) != SYSID_OK) return fail(rc);
+  unsigned epoch = 0;
+  if (streamed) {
+    if (!e->d_in_ready) {
+      HIP_TRY(e, hipMalloc(reinterpret_cast<void**>(&e->d_in_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned)));
+      HIP_TRY(e, hipMemset(e->d_in_ready, 0, (K1_STREAM_ERR + 1) * sizeof(unsigned)));
+      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_in_err), sizeof(unsigned), hipHostMallocDefault));
+    }
+    if (++e->in_epoch == 0) ++e->in_epoch;  // never 0, the flags' initial value
+    epoch = e->in_epoch;
+    *e->h_in_err = 0;
+    if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, ldd, e->stream_parts)) != SYSID_OK) return fail(rc);
+  } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld)) != SYSID_OK) {
+    return fail(rc);
+  }
   // the stacked-output path reads every sample in one launch: all chunks first
   if (staged && !gram_only && (rc = stage_upto(N)) != SYSID_OK) return fail(rc);
   tph[1] = ms_since(t0);  // + buffers, packing started (stacked outputs: every chunk's DMA enqueued)
@@ -1441,9 +1554,19 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     r0 += nrows[k];
   }
-  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
+  const K1Stream kst{e->d_in_ready, (int)stager.chunk(), epoch};
+  rc = streamed  ? launch_gram_chunked(e, e->d_in, N, ldd, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, 0,
+                                       nullptr, &kst)
+       : gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
                                        staged ? stager.chunk() : 0, staged ? &stage_upto : nullptr)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
+  if (streamed) {  // the parts go out after the kernels are queued (and even if a launch failed: K1 must drain)
+    const int rs = stager.send_streamed(e->d_in_ready, epoch);
+    if (rc == SYSID_OK) rc = rs;
+    if (rc == SYSID_OK && hipMemcpyAsync(e->h_in_err, e->d_in_ready + K1_STREAM_ERR, sizeof(unsigned),
+                                         hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = set_err(e, SYSID_E_DEVICE, "stream status copy failed");
+  }
   if (rc != SYSID_OK) return fail(rc);
   if (panel_out) {
     // de-interleave the requested outputs on the device, then one contiguous copy per output
@@ -1480,6 +1603,10 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const hipError_t sst = hipStreamSynchronize(st);
   host_unregister(e, reg);
   tph[3] = ms_since(t0);  // + synchronised
+  if (sst == hipSuccess && streamed && *e->h_in_err) {
+    (void)hipMemset(e->d_in_ready + K1_STREAM_ERR, 0, sizeof(unsigned));
+    return set_err(e, SYSID_E_DEVICE, "streamed inputs: a K1 wave gave up waiting for its part");
+  }
   if (trace)
     std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, launched %.3f, "
                  "done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], tph[2], tph[3]);

@@ -156,7 +156,21 @@ struct K1Params {
   int pov;          // 1: P overlays the projector's working set (wave_layout `pov`)
   double thr_rel;   // rank cut of the projector: remaining row norm <= thr_rel * the largest row norm
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
+  // Streamed inputs (the host entry point's Gram-only path, null otherwise): the input block arrives during the
+  // launch, part p of every claim shard (shard-relative samples [p·in_part, (p+1)·in_part)) flagged by
+  // in_ready[p] reaching in_epoch (written by the copy stream after that part's DMA); in_ready[K1_STREAM_ERR]
+  // is set when a wait gives up.
+  const unsigned* in_ready;
+  int in_part;
+  unsigned in_epoch;
 };
+constexpr int K1_STREAM_ERR = 64;  // in_ready slot of the streamed-input error word (parts < 64)
+
+// Start of claim shard x of N samples: multiples of 16 samples (one 128-byte line of a channel row), so with a
+// 16-sample-aligned row pitch no line of the input block spans two shards or two streamed parts.
+__host__ __device__ inline int64_t k1_shard_begin(int64_t N, int x) {
+  return x >= K1_SHARDS ? N : (N * x / K1_SHARDS) / 16 * 16;
+}
 
 // ------------------------------------------------------------------------------------------------
 // small helpers (host+device so the CPU test-suite can exercise the same code)
@@ -572,7 +586,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   // projector): vmcnt retires in issue order, so consuming them at the top of the next step would first
   // wait for all of this step's panel stores.
   const int home = (int)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (K1_SHARDS - 1));  // XCC_ID
-  auto shard_begin = [&](int x) -> int64_t { return x >= K1_SHARDS ? N : (N * x / K1_SHARDS) / SPW * SPW; };
+  auto shard_begin = [&](int x) -> int64_t { return k1_shard_begin(N, x); };
   int sh = 0;  // shards (counted from home) found exhausted by this wave
   int64_t fnext = f0 + (int64_t)SPW * wave;  // FUSED: the wave's next step in the static deal
   auto claim_issue = [&]() -> unsigned long long {
@@ -622,6 +636,27 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   for (int u = 0; u < NXR; ++u) xr[u] = 0.0;
   auto fetch = [&](int64_t s) {  // s = the step's first sample; this half's is s + half
     const int64_t sh = s + half;
+    if constexpr (!FUSED) {
+      if (kp.in_ready != nullptr && sh < N) {
+        // streamed inputs: wait until this sample's part has landed (its shard, then the part within it).  The
+        // flag is read at system scope (written by the copy stream, not by a shader); the input loads below issue
+        // after the loop exits, and no line they touch was cached before (line-aligned parts, see k1_shard_begin).
+        int x = (int)(sh * K1_SHARDS / N);
+        while (x > 0 && k1_shard_begin(N, x) > sh) --x;
+        while (x + 1 < K1_SHARDS && k1_shard_begin(N, x + 1) <= sh) ++x;
+        const int part = (int)((sh - k1_shard_begin(N, x)) / kp.in_part);
+        int spins = 0;
+        while ((int)(__hip_atomic_load(kp.in_ready + part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - kp.in_epoch) < 0) {
+          __builtin_amdgcn_s_sleep(4);
+          if (++spins > (1 << 22)) {  // ~1 s: report instead of hanging the device
+            __hip_atomic_store(const_cast<unsigned*>(kp.in_ready) + K1_STREAM_ERR, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+        asm volatile("" ::: "memory");
+      }
+    }
 #pragma unroll
     for (int u = 0; u < NXR; ++u)
       if (hl + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hl + HW * u) * ld + sh];
