@@ -158,7 +158,7 @@ struct sysid_engine {
   unsigned* d_in_ready = nullptr;        // host API, streamed inputs: per-part flags + error word (K1Params::in_ready)
   unsigned* h_in_err = nullptr;          // page-locked copy of the error word
   unsigned in_epoch = 0;                 // the flags' value of the current call
-  int stream_parts = 4;                  // parts per claim shard (SYSID_STREAM_PARTS; 0: no streaming)
+  int stream_parts = 0;                  // parts per claim shard (SYSID_STREAM_PARTS; 0: no streaming)
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -300,7 +300,10 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
   kp.out_cols = (int)std::min<int64_t>(ld_panel, prec == 0 ? e->ldp : ld_panel);
   const int64_t waves_needed = (N + spw - 1) / spw;
   const int64_t cap = (int64_t)e->cus * bpc;
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + waves - 1) / waves));
+  // streamed inputs: 8 workgroup slots stay free, because the copy stream's flag writes (hipStreamWriteValue32)
+  // run as blit kernels, which a fully resident K1 waiting for those flags would otherwise never let in
+  const int64_t slots = kst ? std::max<int64_t>(cap / 2, cap - 8) : cap;
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(slots, (waves_needed + waves - 1) / waves));
   const dim3 g1((unsigned)grid), b1(64 * waves);
   // the instantiation unit of (panel type, row mode)
   using K1L = void (*)(int, dim3, dim3, size_t, hipStream_t, const K1Params&, const uint32_t*, const double*, int64_t,
@@ -1526,7 +1529,9 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   unsigned epoch = 0;
   if (streamed) {
     if (!e->d_in_ready) {
-      HIP_TRY(e, hipMalloc(reinterpret_cast<void**>(&e->d_in_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned)));
+      // uncached: the copy stream's flag writes bypass the L2 that K1's polling loads would otherwise keep hitting
+      HIP_TRY(e, hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_in_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned),
+                                       hipDeviceMallocUncached));
       HIP_TRY(e, hipMemset(e->d_in_ready, 0, (K1_STREAM_ERR + 1) * sizeof(unsigned)));
       HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_in_err), sizeof(unsigned), hipHostMallocDefault));
     }
@@ -1604,8 +1609,11 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   host_unregister(e, reg);
   tph[3] = ms_since(t0);  // + synchronised
   if (sst == hipSuccess && streamed && *e->h_in_err) {
+    unsigned fl[4] = {0, 0, 0, 0};
+    (void)hipMemcpy(fl, e->d_in_ready, sizeof fl, hipMemcpyDeviceToHost);
     (void)hipMemset(e->d_in_ready + K1_STREAM_ERR, 0, sizeof(unsigned));
-    return set_err(e, SYSID_E_DEVICE, "streamed inputs: a K1 wave gave up waiting for its part");
+    return set_err(e, SYSID_E_DEVICE, "streamed inputs: a K1 wave gave up waiting for its part (epoch %u, flags %u %u %u %u)",
+                   epoch, fl[0], fl[1], fl[2], fl[3]);
   }
   if (trace)
     std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, launched %.3f, "
