@@ -661,7 +661,8 @@ class Stager {
       if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
       e->pool = new HostPool(T);
     }
-    int parts = 4;  // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few
+    int parts = 2;  // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few
+                    // (Spot 20k Gram-only e2e, 1 / 2 / 4 / 8 chunks: 0.74 / 0.67 / 0.75 / 1.05 ms; profiles/r04_h)
     if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
     CH_ = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
     nch_ = (int)((N_ + CH_ - 1) / CH_);
