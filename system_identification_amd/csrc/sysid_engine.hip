@@ -159,6 +159,7 @@ struct sysid_engine {
   unsigned* h_in_err = nullptr;          // page-locked copy of the error word
   unsigned in_epoch = 0;                 // the flags' value of the current call
   int stream_parts = 0;                  // parts per claim shard (SYSID_STREAM_PARTS; 0: no streaming)
+  int stream_flag_write = 0;             // 1: flags by hipStreamWriteValue32, 0: by a 4-byte DMA (SYSID_STREAM_FLAG)
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -766,8 +767,13 @@ class Stager {
                                       e->copy_stream) != hipSuccess)
           return set_err(e, SYSID_E_DEVICE, "input copy failed");
       }
-      if (hipStreamWriteValue32(e->copy_stream, d_ready + c, epoch, 0) != hipSuccess)
-        return set_err(e, SYSID_E_DEVICE, "input flag write failed");
+      // the flag: a 4-byte copy of the epoch from page-locked memory (the DMA engine, in order after the part's
+      // data), or hipStreamWriteValue32 (SYSID_STREAM_FLAG=write; a blit kernel on this runtime)
+      const hipError_t fr = e->stream_flag_write
+                                ? hipStreamWriteValue32(e->copy_stream, d_ready + c, epoch, 0)
+                                : hipMemcpyAsync(d_ready + c, e->h_in_err + 1, sizeof(unsigned), hipMemcpyHostToDevice,
+                                                 e->copy_stream);
+      if (fr != hipSuccess) return set_err(e, SYSID_E_DEVICE, "input flag write failed");
     }
     return SYSID_OK;
   }
@@ -1101,6 +1107,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SYSID_STREAM_PARTS")) e->stream_parts = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("SYSID_STREAM_FLAG")) e->stream_flag_write = std::strcmp(v, "write") == 0 ? 1 : 0;
   if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   for (int p = 0; p < 3; ++p) {
@@ -1534,11 +1541,12 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
       HIP_TRY(e, hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_in_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned),
                                        hipDeviceMallocUncached));
       HIP_TRY(e, hipMemset(e->d_in_ready, 0, (K1_STREAM_ERR + 1) * sizeof(unsigned)));
-      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_in_err), sizeof(unsigned), hipHostMallocDefault));
+      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_in_err), 2 * sizeof(unsigned), hipHostMallocDefault));
     }
     if (++e->in_epoch == 0) ++e->in_epoch;  // never 0, the flags' initial value
     epoch = e->in_epoch;
-    *e->h_in_err = 0;
+    e->h_in_err[0] = 0;
+    e->h_in_err[1] = epoch;  // the flag value the copy stream sends
     if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, ldd, e->stream_parts)) != SYSID_OK) return fail(rc);
   } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld)) != SYSID_OK) {
     return fail(rc);
