@@ -516,21 +516,28 @@ int gram_nullspace(const sysid_engine* e, uint32_t flags) {
   return want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
 }
 
+// the Gram-only path runs the fused K1 + Gram kernel (K12): f64 projector rows on a model with a K12 form, fusion on
+bool gram_fused(const sysid_engine* e, uint32_t flags) {
+  return gram_prec(flags) == 0 && !gram_nullspace(e, flags) && e->k12_ok && e->fuse;
+}
+
 // staged (host entry point): chunks of at most `staged_chunk` samples, and (*stage_upto)(n) before the K1 of a
 // chunk ending at sample n (it orders `st` after the DMA of the inputs [0, n)); 0 / nullptr: the workspace's chunk
 // size, inputs already on the device.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
                         int64_t staged_chunk = 0, const std::function<int(int64_t)>* stage_upto = nullptr,
-                        const K1Stream* kst = nullptr) {
+                        const K1Stream* kst = nullptr, bool chunk_major = false) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
+  if (chunk_major && (staged_chunk <= 0 || gram_fused(e, flags)))
+    return set_err(e, SYSID_E_INVALID, "chunk-major inputs need the staged, unfused chunk loop");
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
                    gram_ws_bytes_prec(e, N, prec));
   if (reinterpret_cast<uintptr_t>(d_ws) & 255) return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
-  if (prec == 0 && !cmp && e->k12_ok && e->fuse) {
+  if (gram_fused(e, flags)) {
     // fused: K1 + Gram over all N in one launch, the rows through per-wave rings that stay on-die; events as the
     // chunked form's (chunk 0's "K1" = the fused kernel, every other stage 0, then K3)
     double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
@@ -571,14 +578,17 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     const int64_t n = std::min(step, N - c0);
     if (stage_upto && (rc = (*stage_upto)(c0 + n))) return rc;  // this chunk's inputs
     if ((rc = mark())) return rc;
+    // the chunk's input block: row-major samples [c0, c0 + n) of the whole block, or its own (rows x n) block
+    const double* cin = chunk_major ? d_in + (int64_t)e->in_rows * c0 : d_in + c0;
+    const int64_t cld = chunk_major ? n : ld;
     if (cmp) {
-      if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, kst)))
+      if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, kst)))
         return rc;
       const unsigned nseg = (unsigned)((n + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG);
       hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
       hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, rseg, (int)n, e->nv, rowlist, d_rows);
       HIP_TRY(e, hipGetLastError());
-    } else if ((rc = launch_k1(e, d_in + c0, n, ld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr, kst))) {
+    } else if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr, kst))) {
       return rc;
     }
     if ((rc = mark())) return rc;
@@ -644,9 +654,15 @@ class Stager {
   Stager(sysid_engine* e, int64_t N, double* d_dst) : e_(e), N_(N), d_dst_(d_dst) {}
   ~Stager() { finish(); }
   int64_t chunk() const { return CH_; }
+  bool chunk_major() const { return cm_; }
   int chunks() const { return nch_; }
-  int begin(const double* const* srcs, const int* nrows, int nsrc, int64_t ld) {
+  // chunk_major (the Gram-only path, one K1 launch per chunk): chunk c is packed as its own (rows x n) block at
+  // offset rows·c0 of the staging block and of the device block, so it leaves as ONE contiguous DMA, and chunk c's
+  // K1 reads it with ld = n (chunk_input()).  Otherwise the block keeps the caller's row-major layout (ld = N) and
+  // each chunk is a 2-D DMA of one row piece per channel.
+  int begin(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, bool chunk_major = false) {
     sysid_engine* e = e_;
+    cm_ = chunk_major;
     const size_t need = (size_t)e->in_rows * N_ * sizeof(double);
     if (need > e->h_stage_cap) {
       if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -680,7 +696,9 @@ class Stager {
     e->pool->start([this, T, R, hs](int t) {
       for (int c = 0; c < nch_; ++c) {
         const int64_t c0 = c * CH_, n = std::min(CH_, N_ - c0);
-        for (int r = t; r < R; r += T) std::memcpy(hs + (int64_t)r * N_ + c0, row_src_[r] + c0, (size_t)n * sizeof(double));
+        for (int r = t; r < R; r += T)
+          std::memcpy(cm_ ? hs + (int64_t)R * c0 + (int64_t)r * n : hs + (int64_t)r * N_ + c0, row_src_[r] + c0,
+                      (size_t)n * sizeof(double));
         done_[c].fetch_add(1, std::memory_order_release);
       }
     });
@@ -692,14 +710,27 @@ class Stager {
     sysid_engine* e = e_;
     const int T = e->pool->size();
     while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    stamp();  // SYSID_TRACE_HOST: chunk c packed
     const int64_t c0 = c * CH_, n = std::min(CH_, N_ - c0);
     const double* hs = e->h_stage;
-    if (hipMemcpy2DAsync(d_dst_ + c0, (size_t)N_ * sizeof(double), hs + c0, (size_t)N_ * sizeof(double),
-                         (size_t)n * sizeof(double), row_src_.size(), hipMemcpyHostToDevice, e->copy_stream) != hipSuccess ||
-        hipEventRecord(e->stage_ev[c], e->copy_stream) != hipSuccess || hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
+    const int64_t R = (int64_t)row_src_.size();
+    const hipError_t cr =
+        cm_ ? hipMemcpyAsync(d_dst_ + R * c0, hs + R * c0, (size_t)(R * n) * sizeof(double), hipMemcpyHostToDevice,
+                             e->copy_stream)
+            : hipMemcpy2DAsync(d_dst_ + c0, (size_t)N_ * sizeof(double), hs + c0, (size_t)N_ * sizeof(double),
+                               (size_t)n * sizeof(double), (size_t)R, hipMemcpyHostToDevice, e->copy_stream);
+    if (cr != hipSuccess || hipEventRecord(e->stage_ev[c], e->copy_stream) != hipSuccess ||
+        hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
       return set_err(e, SYSID_E_DEVICE, "input copy failed");
+    stamp();  // chunk c's DMA enqueued
     return SYSID_OK;
   }
+  // host-clock stamps (ms since t0) of the trace, two per chunk: packed, DMA enqueued
+  void trace_from(std::chrono::steady_clock::time_point t0) {
+    t0_ = t0;
+    trace_ = true;
+  }
+  const std::vector<double>& stamps() const { return stamps_; }
   void finish() {
     if (started_) e_->pool->wait();
     started_ = false;
@@ -792,6 +823,14 @@ class Stager {
   std::vector<const double*> row_src_;  // channel row r of the block <- its source row
   std::unique_ptr<std::atomic<int>[]> done_;
   bool started_ = false;
+  bool cm_ = false;
+  bool trace_ = false;
+  std::chrono::steady_clock::time_point t0_;
+  std::vector<double> stamps_;
+  void stamp() {
+    if (trace_)
+      stamps_.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0_).count());
+  }
 };
 
 int host_unregister(sysid_engine* e, std::vector<void*>& registered) {
@@ -1502,7 +1541,14 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   // streamed (Gram-only, one chunk, unfused): one K1 launch consumes the inputs as their parts land
   const int gp = gram_prec(flags);
   const bool streamed = staged && gram_only && e->stream_parts > 0 && N <= gram_chunk(e, N, gp) &&
-                        !(gp == 0 && !gram_nullspace(e, flags) && e->k12_ok && e->fuse);
+                        !gram_fused(e, flags);
+  // Gram-only, chunk by chunk: each chunk packed as its own block and sent as one contiguous DMA
+  // (SYSID_STAGE_LAYOUT=rows: the row-major block, a 2-D DMA per chunk)
+  static const bool rows_layout = [] {
+    const char* v = std::getenv("SYSID_STAGE_LAYOUT");
+    return v && std::strcmp(v, "rows") == 0;
+  }();
+  const bool chunk_major = staged && gram_only && !streamed && !gram_fused(e, flags) && !rows_layout;
   const int64_t ldd = streamed ? (N + 15) / 16 * 16 : N;  // device row pitch: whole 128-byte lines when streamed
   int rc;
   if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * ldd * sizeof(double))))
@@ -1526,6 +1572,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
   Stager stager(e, N, e->d_in);
+  if (trace) stager.trace_from(t0);
   int nstaged = 0;  // chunks sent so far
   const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
     for (; nstaged < stager.chunks() && (int64_t)nstaged * stager.chunk() < upto; ++nstaged) {
@@ -1548,7 +1595,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     e->h_in_err[0] = 0;
     e->h_in_err[1] = epoch;  // the flag value the copy stream sends
     if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, ldd, e->stream_parts)) != SYSID_OK) return fail(rc);
-  } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld)) != SYSID_OK) {
+  } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major)) != SYSID_OK) {
     return fail(rc);
   }
   // the stacked-output path reads every sample in one launch: all chunks first
@@ -1572,7 +1619,8 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   rc = streamed  ? launch_gram_chunked(e, e->d_in, N, ldd, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, 0,
                                        nullptr, &kst)
        : gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
-                                       staged ? stager.chunk() : 0, staged ? &stage_upto : nullptr)
+                                       staged ? stager.chunk() : 0, staged ? &stage_upto : nullptr, nullptr,
+                                       chunk_major)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
   if (streamed) {  // the parts go out after the kernels are queued (and even if a launch failed: K1 must drain)
     const int rs = stager.send_streamed(e->d_in_ready, epoch);
@@ -1582,6 +1630,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
       rc = set_err(e, SYSID_E_DEVICE, "stream status copy failed");
   }
   if (rc != SYSID_OK) return fail(rc);
+  const double t_kern = ms_since(t0);  // + kernels enqueued (before the output copies)
   if (panel_out) {
     // de-interleave the requested outputs on the device, then one contiguous copy per output
     const bool wY = Y_proj && (flags & SYSID_EMIT_Y), wT = tau_proj && (flags & SYSID_EMIT_TAU);
@@ -1625,8 +1674,18 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
                    epoch, fl[0], fl[1], fl[2], fl[3]);
   }
   if (trace)
-    std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, launched %.3f, "
-                 "done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], tph[2], tph[3]);
+    std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, kernels enqueued "
+                 "%.3f, launched %.3f, done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], t_kern, tph[2],
+                 tph[3]);
+  if (trace && !stager.stamps().empty()) {
+    std::string line = "  chunk stamps (packed, DMA enqueued) ms:";
+    char buf[32];
+    for (double x : stager.stamps()) {
+      std::snprintf(buf, sizeof buf, " %.3f", x);
+      line += buf;
+    }
+    std::fprintf(stderr, "%s\n", line.c_str());
+  }
   if (sst != hipSuccess) return set_err(e, SYSID_E_DEVICE, "stream sync failed: %s", hipGetErrorString(sst));
   return SYSID_OK;
 }

@@ -327,6 +327,29 @@ def test_gram_only_chunked(robot, N):
         e.set_gram_chunk_bytes(1000)
 
 
+@pytest.mark.parametrize("robot,N,chunks", [("spot", 20001, 3), ("spot", 4999, 2), ("g1_29dof", 3001, 4)])
+def test_host_gram_only_staged_chunks(robot, N, chunks, monkeypatch):
+    """Host Gram-only entry point with its inputs staged in `chunks` chunk-major blocks (each chunk packed as its
+    own block and sent as one DMA, its K1 reading it with ld = the chunk's length), ragged last chunk: the same
+    normal equations as the device entry point on the row-major block, to rounding."""
+    import torch
+    monkeypatch.setenv("SYSID_STAGE_CHUNKS", str(chunks))
+    model = load_robot(robot)
+    e = Engine(model)
+    d = generate(model, N, config_index=4)
+    only = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_GRAM)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    bufs = e.alloc_gram_device(N)
+    e.build_gram_device(din, N, bufs)
+    torch.cuda.synchronize()
+    W = e.w
+    G = bufs["gram"].cpu().numpy()
+    assert rel(only["gram"], G[:W, :W]) < 1e-12
+    assert rel(only["Atb"], G[:W, W]) < 1e-12
+    assert abs(only["btb"] - G[W, W]) <= 1e-12 * abs(G[W, W])
+    assert only["num_rows"] == N * model.nv
+
+
 @pytest.mark.parametrize("robot,N", [("spot", 3000), ("g1_29dof", 700)])
 def test_tau_prediction_rmse_reduction(robot, N):
     """K4 (device reduction of the torque-prediction error) against the reference's loop over the
