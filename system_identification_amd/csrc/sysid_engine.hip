@@ -574,13 +574,17 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     return SYSID_OK;
   };
   const int64_t step = staged_chunk > 0 && staged_chunk < C ? staged_chunk : C;
-  for (int64_t c0 = 0; c0 < N; c0 += step) {
-    const int64_t n = std::min(step, N - c0);
+  for (int64_t c0 = 0, n = 0; c0 < N; c0 += n) {
+    n = std::min(step, N - c0);
+    // chunk-major inputs: staged chunk k = [k0, k1) is its own (rows x (k1 - k0)) block at offset rows·k0; a
+    // launch never straddles two of them (a staged chunk larger than the workspace chunk runs as several)
+    const int64_t k0 = chunk_major ? c0 / staged_chunk * staged_chunk : 0;
+    const int64_t k1 = chunk_major ? std::min(k0 + staged_chunk, N) : N;
+    if (chunk_major) n = std::min(n, k1 - c0);
     if (stage_upto && (rc = (*stage_upto)(c0 + n))) return rc;  // this chunk's inputs
     if ((rc = mark())) return rc;
-    // the chunk's input block: row-major samples [c0, c0 + n) of the whole block, or its own (rows x n) block
-    const double* cin = chunk_major ? d_in + (int64_t)e->in_rows * c0 : d_in + c0;
-    const int64_t cld = chunk_major ? n : ld;
+    const double* cin = chunk_major ? d_in + (int64_t)e->in_rows * k0 + (c0 - k0) : d_in + c0;
+    const int64_t cld = chunk_major ? k1 - k0 : ld;
     if (cmp) {
       if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, kst)))
         return rc;

@@ -327,15 +327,19 @@ def test_gram_only_chunked(robot, N):
         e.set_gram_chunk_bytes(1000)
 
 
-@pytest.mark.parametrize("robot,N,chunks", [("spot", 20001, 3), ("spot", 4999, 2), ("g1_29dof", 3001, 4)])
-def test_host_gram_only_staged_chunks(robot, N, chunks, monkeypatch):
+@pytest.mark.parametrize("robot,N,chunks,ws_chunk", [("spot", 20001, 3, 0), ("spot", 4999, 2, 0), ("g1_29dof", 3001, 4, 0),
+                                                    ("spot", 20001, 2, 8 << 20), ("g1_29dof", 3001, 2, 16 << 20)])
+def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
     """Host Gram-only entry point with its inputs staged in `chunks` chunk-major blocks (each chunk packed as its
-    own block and sent as one DMA, its K1 reading it with ld = the chunk's length), ragged last chunk: the same
+    own block and sent as one DMA, its K1 reading it with ld = the chunk's length), ragged last chunk, and staged
+    chunks larger than the workspace's panel chunk (ws_chunk bytes: several K1 launches per staged block): the same
     normal equations as the device entry point on the row-major block, to rounding."""
     import torch
     monkeypatch.setenv("SYSID_STAGE_CHUNKS", str(chunks))
     model = load_robot(robot)
     e = Engine(model)
+    if ws_chunk:
+        e.set_gram_chunk_bytes(ws_chunk)
     d = generate(model, N, config_index=4)
     only = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_GRAM)
     din = torch.from_numpy(channel_block(d)).cuda()
