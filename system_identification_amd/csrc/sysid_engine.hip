@@ -155,11 +155,12 @@ struct sysid_engine {
   size_t h_stage_cap = 0;
   HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
   hipStream_t copy_stream = nullptr;     // host API: the staged input chunks' DMA (created on first use)
-  unsigned* d_in_ready = nullptr;        // host API, streamed inputs: per-part flags + error word (K1Params::in_ready)
-  unsigned* h_in_err = nullptr;          // page-locked copy of the error word
+  unsigned* h_ready = nullptr;           // host API, streamed inputs: per-part flags + error word in coherent host
+                                         // memory (K1Params::in_ready), written by the host
+  double* d_in_uc = nullptr;             // streamed inputs: the part-major device block (uncached, grow-only)
+  size_t in_uc_cap = 0;
   unsigned in_epoch = 0;                 // the flags' value of the current call
   int stream_parts = 0;                  // parts per claim shard (SYSID_STREAM_PARTS; 0: no streaming)
-  int stream_flag_write = 0;             // 1: flags by hipStreamWriteValue32, 0: by a 4-byte DMA (SYSID_STREAM_FLAG)
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -301,10 +302,9 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
   kp.out_cols = (int)std::min<int64_t>(ld_panel, prec == 0 ? e->ldp : ld_panel);
   const int64_t waves_needed = (N + spw - 1) / spw;
   const int64_t cap = (int64_t)e->cus * bpc;
-  // streamed inputs: 8 workgroup slots stay free, because the copy stream's flag writes (hipStreamWriteValue32)
-  // run as blit kernels, which a fully resident K1 waiting for those flags would otherwise never let in
-  const int64_t slots = kst ? std::max<int64_t>(cap / 2, cap - 8) : cap;
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(slots, (waves_needed + waves - 1) / waves));
+  // (streamed inputs: the copies are copy-engine DMAs and the flags host stores, so a full grid never waits on
+  // a kernel that cannot become resident)
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + waves - 1) / waves));
   const dim3 g1((unsigned)grid), b1(64 * waves);
   // the instantiation unit of (panel type, row mode)
   using K1L = void (*)(int, dim3, dim3, size_t, hipStream_t, const K1Params&, const uint32_t*, const double*, int64_t,
@@ -653,6 +653,24 @@ int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemc
 // chunk; the stacked-output path stages every chunk before its single K1).  Measured on Spot 20k Gram-only: the
 // pack-everything-first form took 0.19 ms of packing before the first kernel (profiles/r04_g).  The staging block
 // is reused by the next call only after this call's launch-stream synchronise, which follows every DMA.
+// The host entry points' copy stream, created on first use and warmed by one small DMA: the runtime sets up the
+// stream's copy queue lazily on its first copy, which under a resident full-chip K1 took milliseconds
+// (profiles/r04_s3: the first streamed call's first part started 8 ms after K1).
+int ensure_copy_stream(sysid_engine* e) {
+  if (e->copy_stream) return SYSID_OK;
+  HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+  double* h = nullptr;
+  HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&h), 256, hipHostMallocDefault));
+  double* d = nullptr;
+  hipError_t r = hipMalloc(reinterpret_cast<void**>(&d), 256);
+  if (r == hipSuccess) r = hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, e->copy_stream);
+  if (r == hipSuccess) r = hipStreamSynchronize(e->copy_stream);
+  if (d) (void)hipFree(d);
+  (void)hipHostFree(h);
+  if (r != hipSuccess) return set_err(e, SYSID_E_DEVICE, "copy stream set-up failed: %s", hipGetErrorString(r));
+  return SYSID_OK;
+}
+
 class Stager {
  public:
   Stager(sysid_engine* e, int64_t N, double* d_dst) : e_(e), N_(N), d_dst_(d_dst) {}
@@ -687,7 +705,7 @@ class Stager {
     if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
     CH_ = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
     nch_ = (int)((N_ + CH_ - 1) / CH_);
-    if (!e->copy_stream) HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+    if (int rc = ensure_copy_stream(e)) return rc;
     while ((int)e->stage_ev.size() < nch_) {
       hipEvent_t x;
       HIP_TRY(e, hipEventCreateWithFlags(&x, hipEventDisableTiming));
@@ -741,14 +759,30 @@ class Stager {
   }
 
   // Streamed form (the Gram-only path when it is one chunk: ONE K1 launch over all N whose waves wait per part,
-  // K1Params::in_ready): the device block's row pitch is `ldd` (a multiple of 16 samples), and part p is the
-  // shard-relative samples [p·PL, (p+1)·PL) of every claim shard (k1_shard_begin), so the K1 waves of every XCD
-  // start on part 0 together.  Packed part by part; send_streamed() then sends part p as one 2-D DMA per shard
-  // piece and flags it (in_ready[p] = epoch, written by the copy stream after those DMAs).
-  int begin_streamed(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, int64_t ldd, int parts) {
+  // K1Params::in_ready).  Part p is the shard-relative samples [p·PL, (p+1)·PL) of every claim shard
+  // (k1_shard_begin), so the K1 waves of every XCD start on part 0 together; it is packed part-major — piece (p,
+  // shard x) = R rows x PL samples at offset (p·K1_SHARDS + x)·R·PL — and leaves as ONE contiguous DMA.
+  // send_streamed() enqueues the parts' DMAs with an event each; flag_streamed() then writes in_ready[p] = epoch in
+  // host memory as each DMA completes.
+  static int64_t part_len(int64_t N, int parts) {
+    int64_t maxlen = 0;
+    for (int x = 0; x < K1_SHARDS; ++x) maxlen = std::max(maxlen, k1_shard_begin(N, x + 1) - k1_shard_begin(N, x));
+    parts = std::max(1, std::min(parts, K1_STREAM_ERR));
+    return std::max<int64_t>(16, ((maxlen + parts - 1) / parts + 15) / 16 * 16);  // whole 128-byte lines
+  }
+  static int part_count(int64_t N, int64_t PL) {
+    int64_t maxlen = 0;
+    for (int x = 0; x < K1_SHARDS; ++x) maxlen = std::max(maxlen, k1_shard_begin(N, x + 1) - k1_shard_begin(N, x));
+    return (int)std::max<int64_t>(1, (maxlen + PL - 1) / PL);
+  }
+  int begin_streamed(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, int parts) {
     sysid_engine* e = e_;
-    ldd_ = ldd;
-    const size_t need = (size_t)e->in_rows * ldd * sizeof(double);
+    CH_ = part_len(N_, parts);
+    nch_ = part_count(N_, CH_);
+    for (int k = 0; k < nsrc; ++k)
+      for (int r = 0; r < nrows[k]; ++r) row_src_.push_back(srcs[k] + (int64_t)r * ld);
+    const int64_t R = (int64_t)row_src_.size();
+    const size_t need = (size_t)nch_ * K1_SHARDS * R * CH_ * sizeof(double);
     if (need > e->h_stage_cap) {
       if (e->h_stage) (void)hipHostFree(e->h_stage);
       e->h_stage = nullptr;
@@ -756,31 +790,30 @@ class Stager {
       HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
       e->h_stage_cap = need;
     }
-    for (int k = 0; k < nsrc; ++k)
-      for (int r = 0; r < nrows[k]; ++r) row_src_.push_back(srcs[k] + (int64_t)r * ld);
     if (!e->pool) {
       int T = 8;
       if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
       e->pool = new HostPool(T);
     }
-    int64_t maxlen = 0;
-    for (int x = 0; x < K1_SHARDS; ++x) maxlen = std::max(maxlen, k1_shard_begin(N_, x + 1) - k1_shard_begin(N_, x));
-    parts = std::max(1, std::min(parts, K1_STREAM_ERR));
-    CH_ = std::max<int64_t>(16, ((maxlen + parts - 1) / parts + 15) / 16 * 16);  // PL: whole 128-byte lines
-    nch_ = (int)std::max<int64_t>(1, (maxlen + CH_ - 1) / CH_);
-    if (!e->copy_stream) HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+    if (int rc = ensure_copy_stream(e)) return rc;
+    while ((int)e->stage_ev.size() < nch_) {
+      hipEvent_t x;
+      HIP_TRY(e, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      e->stage_ev.push_back(x);
+    }
     done_.reset(new std::atomic<int>[nch_]);
     for (int c = 0; c < nch_; ++c) done_[c].store(0);
-    const int T = e->pool->size(), R = (int)row_src_.size();
+    const int T = e->pool->size();
     double* hs = e->h_stage;
     e->pool->start([this, T, R, hs](int t) {
       for (int c = 0; c < nch_; ++c) {
         for (int x = 0; x < K1_SHARDS; ++x) {
           int64_t c0, n;
           piece(c, x, &c0, &n);
+          double* blk = hs + ((int64_t)c * K1_SHARDS + x) * R * CH_;
           if (n > 0)
-            for (int r = t; r < R; r += T)
-              std::memcpy(hs + (int64_t)r * ldd_ + c0, row_src_[r] + c0, (size_t)n * sizeof(double));
+            for (int64_t r = t; r < R; r += T)
+              std::memcpy(blk + r * CH_, row_src_[r] + c0, (size_t)n * sizeof(double));
         }
         done_[c].fetch_add(1, std::memory_order_release);
       }
@@ -788,29 +821,37 @@ class Stager {
     started_ = true;
     return SYSID_OK;
   }
-  int send_streamed(unsigned* d_ready, unsigned epoch) {
+  size_t streamed_bytes() const { return (size_t)nch_ * K1_SHARDS * row_src_.size() * CH_ * sizeof(double); }
+  int send_streamed() {
     sysid_engine* e = e_;
     const int T = e->pool->size();
-    const double* hs = e->h_stage;
+    const size_t pb = (size_t)K1_SHARDS * row_src_.size() * CH_;  // doubles per part
     for (int c = 0; c < nch_; ++c) {
       while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
-      for (int x = 0; x < K1_SHARDS; ++x) {
-        int64_t c0, n;
-        piece(c, x, &c0, &n);
-        if (n > 0 && hipMemcpy2DAsync(d_dst_ + c0, (size_t)ldd_ * sizeof(double), hs + c0, (size_t)ldd_ * sizeof(double),
-                                      (size_t)n * sizeof(double), row_src_.size(), hipMemcpyHostToDevice,
-                                      e->copy_stream) != hipSuccess)
-          return set_err(e, SYSID_E_DEVICE, "input copy failed");
-      }
-      // the flag: a 4-byte copy of the epoch from page-locked memory (the DMA engine, in order after the part's
-      // data), or hipStreamWriteValue32 (SYSID_STREAM_FLAG=write; a blit kernel on this runtime)
-      const hipError_t fr = e->stream_flag_write
-                                ? hipStreamWriteValue32(e->copy_stream, d_ready + c, epoch, 0)
-                                : hipMemcpyAsync(d_ready + c, e->h_in_err + 1, sizeof(unsigned), hipMemcpyHostToDevice,
-                                                 e->copy_stream);
-      if (fr != hipSuccess) return set_err(e, SYSID_E_DEVICE, "input flag write failed");
+      stamp();
+      if (hipMemcpyAsync(d_dst_ + c * pb, e->h_stage + c * pb, pb * sizeof(double), hipMemcpyHostToDevice,
+                         e->copy_stream) != hipSuccess ||
+          hipEventRecord(e->stage_ev[c], e->copy_stream) != hipSuccess)
+        return set_err(e, SYSID_E_DEVICE, "input copy failed");
     }
     return SYSID_OK;
+  }
+  // in_ready[c] = epoch as part c's DMA completes (every flag is written, also after an error, so K1 drains)
+  // (bounded: a DMA not done 2 s after the call began is reported, and its flag written anyway so K1 drains)
+  int flag_streamed(unsigned* h_ready, unsigned epoch) {
+    int rc = SYSID_OK;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+    for (int c = 0; c < nch_; ++c) {
+      hipError_t q;
+      while ((q = hipEventQuery(e_->stage_ev[c])) == hipErrorNotReady && std::chrono::steady_clock::now() < deadline)
+        std::this_thread::yield();
+      if (q != hipSuccess && rc == SYSID_OK)
+        rc = set_err(e_, SYSID_E_DEVICE, "streamed inputs: part %d of %d: %s", c, nch_,
+                     q == hipErrorNotReady ? "its DMA had not completed after 2 s" : hipGetErrorString(q));
+      __atomic_store_n(h_ready + c, epoch, __ATOMIC_SEQ_CST);
+      stamp();
+    }
+    return rc;
   }
 
  private:
@@ -821,7 +862,7 @@ class Stager {
   }
 
   sysid_engine* e_;
-  int64_t N_, CH_ = 0, ldd_ = 0;
+  int64_t N_, CH_ = 0;
   int nch_ = 0;
   double* d_dst_;
   std::vector<const double*> row_src_;  // channel row r of the block <- its source row
@@ -1150,7 +1191,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SYSID_STREAM_PARTS")) e->stream_parts = std::max(0, std::atoi(v));
-  if (const char* v = std::getenv("SYSID_STREAM_FLAG")) e->stream_flag_write = std::strcmp(v, "write") == 0 ? 1 : 0;
   if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   for (int p = 0; p < 3; ++p) {
@@ -1250,8 +1290,8 @@ void sysid_destroy(sysid_engine* e) {
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   delete e->pool;
   for (hipEvent_t x : e->stage_ev) (void)hipEventDestroy(x);
-  if (e->d_in_ready) (void)hipFree(e->d_in_ready);
-  if (e->h_in_err) (void)hipHostFree(e->h_in_err);
+  if (e->h_ready) (void)hipHostFree(e->h_ready);
+  if (e->d_in_uc) (void)hipFree(e->d_in_uc);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -1553,10 +1593,20 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     return v && std::strcmp(v, "rows") == 0;
   }();
   const bool chunk_major = staged && gram_only && !streamed && !gram_fused(e, flags) && !rows_layout;
-  const int64_t ldd = streamed ? (N + 15) / 16 * 16 : N;  // device row pitch: whole 128-byte lines when streamed
   int rc;
-  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * ldd * sizeof(double))))
+  if (streamed) {  // the part-major device block, uncached (grow-only)
+    const int64_t PL = Stager::part_len(N, e->stream_parts);
+    const size_t need = (size_t)Stager::part_count(N, PL) * K1_SHARDS * e->in_rows * PL * sizeof(double);
+    if (need > e->in_uc_cap) {
+      if (e->d_in_uc) (void)hipFree(e->d_in_uc);
+      e->d_in_uc = nullptr;
+      e->in_uc_cap = 0;
+      HIP_TRY(e, hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_in_uc), need, hipDeviceMallocUncached));
+      e->in_uc_cap = need;
+    }
+  } else if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) {
     return rc;
+  }
   if (!gram_only &&
       (rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
     return rc;
@@ -1575,7 +1625,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   // host threads for blocks of 1 MiB and more (stage_inputs), else one copy per array
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
-  Stager stager(e, N, e->d_in);
+  Stager stager(e, N, streamed ? e->d_in_uc : e->d_in);
   if (trace) stager.trace_from(t0);
   int nstaged = 0;  // chunks sent so far
   const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
@@ -1587,18 +1637,16 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   };
   unsigned epoch = 0;
   if (streamed) {
-    if (!e->d_in_ready) {
-      // uncached: the copy stream's flag writes bypass the L2 that K1's polling loads would otherwise keep hitting
-      HIP_TRY(e, hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_in_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned),
-                                       hipDeviceMallocUncached));
-      HIP_TRY(e, hipMemset(e->d_in_ready, 0, (K1_STREAM_ERR + 1) * sizeof(unsigned)));
-      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_in_err), 2 * sizeof(unsigned), hipHostMallocDefault));
+    if (!e->h_ready) {
+      // coherent host memory: the host's stores reach K1's system-scope polling loads while K1 runs
+      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned),
+                               hipHostMallocCoherent));
+      std::memset(e->h_ready, 0, (K1_STREAM_ERR + 1) * sizeof(unsigned));
     }
     if (++e->in_epoch == 0) ++e->in_epoch;  // never 0, the flags' initial value
     epoch = e->in_epoch;
-    e->h_in_err[0] = 0;
-    e->h_in_err[1] = epoch;  // the flag value the copy stream sends
-    if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, ldd, e->stream_parts)) != SYSID_OK) return fail(rc);
+    __atomic_store_n(e->h_ready + K1_STREAM_ERR, 0u, __ATOMIC_SEQ_CST);
+    if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, e->stream_parts)) != SYSID_OK) return fail(rc);
   } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major)) != SYSID_OK) {
     return fail(rc);
   }
@@ -1619,19 +1667,18 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     r0 += nrows[k];
   }
-  const K1Stream kst{e->d_in_ready, (int)stager.chunk(), epoch};
-  rc = streamed  ? launch_gram_chunked(e, e->d_in, N, ldd, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, 0,
+  const K1Stream kst{e->h_ready, (int)stager.chunk(), epoch};
+  rc = streamed  ? launch_gram_chunked(e, e->d_in_uc, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, 0,
                                        nullptr, &kst)
        : gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
                                        staged ? stager.chunk() : 0, staged ? &stage_upto : nullptr, nullptr,
                                        chunk_major)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
-  if (streamed) {  // the parts go out after the kernels are queued (and even if a launch failed: K1 must drain)
-    const int rs = stager.send_streamed(e->d_in_ready, epoch);
+  if (streamed) {  // the parts go out after the kernels are queued, and every flag is written (K1 must drain)
+    const int rs = stager.send_streamed();
     if (rc == SYSID_OK) rc = rs;
-    if (rc == SYSID_OK && hipMemcpyAsync(e->h_in_err, e->d_in_ready + K1_STREAM_ERR, sizeof(unsigned),
-                                         hipMemcpyDeviceToHost, st) != hipSuccess)
-      rc = set_err(e, SYSID_E_DEVICE, "stream status copy failed");
+    const int rf = stager.flag_streamed(e->h_ready, epoch);
+    if (rc == SYSID_OK) rc = rf;
   }
   if (rc != SYSID_OK) return fail(rc);
   const double t_kern = ms_since(t0);  // + kernels enqueued (before the output copies)
@@ -1670,10 +1717,8 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const hipError_t sst = hipStreamSynchronize(st);
   host_unregister(e, reg);
   tph[3] = ms_since(t0);  // + synchronised
-  if (sst == hipSuccess && streamed && *e->h_in_err) {
-    unsigned fl[4] = {0, 0, 0, 0};
-    (void)hipMemcpy(fl, e->d_in_ready, sizeof fl, hipMemcpyDeviceToHost);
-    (void)hipMemset(e->d_in_ready + K1_STREAM_ERR, 0, sizeof(unsigned));
+  if (sst == hipSuccess && streamed && __atomic_load_n(e->h_ready + K1_STREAM_ERR, __ATOMIC_SEQ_CST)) {
+    const unsigned* fl = e->h_ready;
     return set_err(e, SYSID_E_DEVICE, "streamed inputs: a K1 wave gave up waiting for its part (epoch %u, flags %u %u %u %u)",
                    epoch, fl[0], fl[1], fl[2], fl[3]);
   }

@@ -157,8 +157,10 @@ struct K1Params {
   double thr_rel;   // rank cut of the projector: remaining row norm <= thr_rel * the largest row norm
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
   // Streamed inputs (the host entry point's Gram-only path, null otherwise): the input block arrives during the
-  // launch, part p of every claim shard (shard-relative samples [p·in_part, (p+1)·in_part)) flagged by
-  // in_ready[p] reaching in_epoch (written by the copy stream after that part's DMA); in_ready[K1_STREAM_ERR]
+  // launch in part-major order — part p = the shard-relative samples [p·in_part, (p+1)·in_part) of every claim
+  // shard, one DMA — and part p is flagged by in_ready[p] reaching in_epoch.  in_ready lives in coherent host
+  // memory and is written by the host once the part's DMA has completed (a copy engine's or blit kernel's flag
+  // write on another stream does not progress while a full-chip kernel spins: profiles/r04_s3); in_ready[K1_STREAM_ERR]
   // is set when a wait gives up.
   const unsigned* in_ready;
   int in_part;
@@ -636,19 +638,26 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   for (int u = 0; u < NXR; ++u) xr[u] = 0.0;
   auto fetch = [&](int64_t s) {  // s = the step's first sample; this half's is s + half
     const int64_t sh = s + half;
+    // channel c of the sample at in[ib + c·is]: the row-major block (ib = sh, is = ld) or, streamed, the sample's
+    // column of its (part, shard) piece of the part-major block (is = in_part)
+    int64_t ib = sh, is = ld;
     if constexpr (!FUSED) {
       if (kp.in_ready != nullptr && sh < N) {
         // streamed inputs: wait until this sample's part has landed (its shard, then the part within it).  The
-        // flag is read at system scope (written by the copy stream, not by a shader); the input loads below issue
-        // after the loop exits, and no line they touch was cached before (line-aligned parts, see k1_shard_begin).
+        // flag is read at system scope (host memory written by the host); the input loads below issue after the
+        // loop exits, from an uncached device block (no L2 line of an earlier call's inputs can be hit).
         int x = (int)(sh * K1_SHARDS / N);
         while (x > 0 && k1_shard_begin(N, x) > sh) --x;
         while (x + 1 < K1_SHARDS && k1_shard_begin(N, x + 1) <= sh) ++x;
-        const int part = (int)((sh - k1_shard_begin(N, x)) / kp.in_part);
-        int spins = 0;
+        const int64_t so = sh - k1_shard_begin(N, x);
+        const int part = (int)(so / kp.in_part);
+        // part-major block: (part, shard) pieces of IN rows x in_part samples each, one DMA per part
+        ib = ((int64_t)(part * K1_SHARDS + x) * IN) * kp.in_part + (so - (int64_t)part * kp.in_part);
+        is = kp.in_part;
+        const uint64_t t_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
         while ((int)(__hip_atomic_load(kp.in_ready + part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - kp.in_epoch) < 0) {
           __builtin_amdgcn_s_sleep(4);
-          if (++spins > (1 << 22)) {  // ~1 s: report instead of hanging the device
+          if (__builtin_amdgcn_s_memrealtime() - t_start > 100000000ull) {  // 1 s: report instead of hanging the device
             __hip_atomic_store(const_cast<unsigned*>(kp.in_ready) + K1_STREAM_ERR, 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             break;
@@ -659,7 +668,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     }
 #pragma unroll
     for (int u = 0; u < NXR; ++u)
-      if (hl + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hl + HW * u) * ld + sh];
+      if (hl + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hl + HW * u) * is + ib];
   };
   double* sin_ = wr + L.in;
   const double* q = sin_;
