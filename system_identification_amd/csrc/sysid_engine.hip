@@ -231,9 +231,10 @@ bool k1_is_pov(int variant) { return variant == K1_C12P || variant == K1_C16P; }
 int k1_chain_slots(int maxch) { return maxch <= 4 ? 4 : maxch <= 12 ? 12 : 16; }
 
 // maxch: the longest revolute chain.  The nv = 18 kernel unrolls SYSID_K1_QCH chain slots.
-int k1_variant(int maxch, int nv, int nbody) {
-  // the nv = 18 kernel stages two panel rows of all bodies (lane = body x row group: 11..16 bodies)
-  if (maxch <= SYSID_K1_QCH && nv == 18 && nbody >= 11 && nbody <= 16) return K1_C4_NV18;
+int k1_variant(int maxch, int nv, int nbody, int in_lds) {
+  // the nv = 18 kernel stages two panel rows of all bodies (lane = body x row group: 11..16 bodies) and prefetches
+  // at most K1_QUAD_IN_MAX input channels (its registers are sized for them)
+  if (maxch <= SYSID_K1_QCH && nv == 18 && nbody >= 11 && nbody <= 16 && in_lds <= K1_QUAD_IN_MAX) return K1_C4_NV18;
   return maxch <= 4 ? K1_C4 : k1_chain_slots(maxch) == 12 ? K1_C12 : K1_C16;
 }
 
@@ -1014,7 +1015,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->ldp = (e->ncol + 1) & ~1;
   e->in_rows = in_rows;
   e->in_lds = in_lds;
-  const int v0 = k1_variant(maxch, nv, NJ - 1);
+  const int v0 = k1_variant(maxch, nv, NJ - 1, in_lds);
   const int lhw = k1_layout_hw(v0);
   const WLay WL0 = wave_layout(in_lds, nv, NJ, nc, lhw);
   // P overlay (wave_layout `pov`): runtime-nv kernels whose H1 is read from P (an even free-flyer offset), when

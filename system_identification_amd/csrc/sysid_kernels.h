@@ -166,6 +166,7 @@ struct K1Params {
   int in_part;
   unsigned in_epoch;
 };
+constexpr int K1_QUAD_IN_MAX = 96;  // input channels of the quadruped K1 (nv = 18, two samples per wave)
 constexpr int K1_STREAM_ERR = 64;  // in_ready slot of the streamed-input error word (parts < 64)
 
 // Start of claim shard x of N samples: multiples of 16 samples (one 128-byte line of a channel row), so with a
@@ -632,7 +633,9 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     }
     return N;
   };
-  constexpr int NXR = (192 + HW - 1) / HW;  // input registers per lane (<= 192 channels)
+  // input registers per lane: <= 192 channels, the quadruped kernel <= K1_QUAD_IN_MAX (host-checked, k1_variant:
+  // its 6 prefetch registers for 192 had held 6 dead VGPRs across every step of a 71-channel Spot sample)
+  constexpr int NXR = ((NVC == 18 && HW == 32 ? K1_QUAD_IN_MAX : 192) + HW - 1) / HW;
   double xr[NXR];
 #pragma unroll
   for (int u = 0; u < NXR; ++u) xr[u] = 0.0;
