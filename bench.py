@@ -346,6 +346,23 @@ def main():
                   "samples_per_s": round(total_per_step * args.steps / el2, 1),
                   "settle": pre, "note": "the same K steps re-timed after 250 ms of untimed back-to-back steps "
                                          "(clocks at their operating point); not the headline value"}
+    # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only: the chunked
+    # path itself, each stage summed over its chunks.  Measured right after the timed region and the steady-state
+    # re-timing, before the host-entry-point legs (whose host-bound gaps let the clocks drop again), so it sees the
+    # kernels at the clocks rocprofv3's average over the same run sees them.
+    n_time = N
+    fused = eng.fused(tflags & ~0x7 if args.gram_only else flags)  # K12: K1 + Gram in one launch (ms[1] = 0)
+    ms = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
+    ms_unfused, ms_fused = None, None
+    if fused:  # the same stages with fusion off, for the record (K1 -> K2 -> K3 as three launches)
+        eng.set_fusion(False)
+        ms_unfused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
+        eng.set_fusion(True)
+    else:  # fusion off (the default: measured slower), the fused kernel's time for the record where it exists
+        eng.set_fusion(True)
+        if eng.fused(tflags & ~0x7 if args.gram_only else flags):
+            ms_fused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
+        eng.set_fusion(False)
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = e2e_legs(eng, data, N)
@@ -372,21 +389,6 @@ def main():
         exchange_check["num_rows"] = float(xbuf[-1].item())
         exchange_check["num_rows_ok"] = exchange_check["num_rows"] == float(total_per_step * model.nv)
 
-    # per-kernel device time (HIP events on the engine's stream), for the roofline.  Gram-only: the chunked
-    # path itself, each stage summed over its chunks.
-    n_time = N
-    fused = eng.fused(tflags & ~0x7 if args.gram_only else flags)  # K12: K1 + Gram in one launch (ms[1] = 0)
-    ms = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-    ms_unfused, ms_fused = None, None
-    if fused:  # the same stages with fusion off, for the record (K1 -> K2 -> K3 as three launches)
-        eng.set_fusion(False)
-        ms_unfused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-        eng.set_fusion(True)
-    else:  # fusion off (the default: measured slower), the fused kernel's time for the record where it exists
-        eng.set_fusion(True)
-        if eng.fused(tflags & ~0x7 if args.gram_only else flags):
-            ms_fused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-        eng.set_fusion(False)
     nv, W = model.nv, eng.w
     in_b = (model.nq + 2 * nv + model.nj + model.n_ee) * 8
     esize = {"f64": 8, "f32": 4, "bf16": 2}[args.precision] if args.gram_only else 8
