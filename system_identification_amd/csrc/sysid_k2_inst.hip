@@ -10,6 +10,12 @@
 #error "SYSID_WIDE (0: 1..15 tile columns, 1: 16..24) must be set"
 #endif
 
+// rows per staged chunk of the 10-tile-column narrow Gram (Spot, solo12): 24 (K2 0.1640 ms) against 16 / 32 / 40 / 48
+// (0.1662 / 0.1650 / slower / slower; profiles/r04_s8, r03_l); -D for A/B builds only
+#ifndef SYSID_K2_KC10
+#define SYSID_K2_KC10 24
+#endif
+
 namespace sysid_launch {
 using namespace sysid_dev;
 
@@ -84,7 +90,7 @@ bool k2_launch(const K2Args& a) {
     SYSID_K2_CASE(21, 8) SYSID_K2_CASE(22, 8) SYSID_K2_CASE(23, 8) SYSID_K2_CASE(24, 8)
 #else
     SYSID_K2_CASE(1, 32) SYSID_K2_CASE(2, 32) SYSID_K2_CASE(3, 32) SYSID_K2_CASE(4, 32) SYSID_K2_CASE(5, 32)
-    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, 32)
+    SYSID_K2_CASE(6, 32) SYSID_K2_CASE(7, 32) SYSID_K2_CASE(8, 32) SYSID_K2_CASE(9, 32) SYSID_K2_CASE(10, SYSID_K2_KC10)
     SYSID_K2_CASE(11, 24) SYSID_K2_CASE(12, 24) SYSID_K2_CASE(13, 24) SYSID_K2_CASE(14, 20) SYSID_K2_CASE(15, 20)
 #endif
     default: return false;
