@@ -517,22 +517,29 @@ int gram_nullspace(const sysid_engine* e, uint32_t flags) {
   return want_ns && 3 * e->nc <= K1_CMP_KMAX ? 1 : 0;
 }
 
+// samples one round of K1 takes: every resident wave one step (Spot: 256 CUs x 2 workgroups x 4 waves x 2 samples)
+int64_t k1_round_samples(const sysid_engine* e, int prec, int cmp) {
+  const sysid_engine::K1Shape& K = cmp ? e->k1c[prec] : e->k1m[prec];
+  return (int64_t)e->cus * K.bpc * K.waves * k1_spw(K.variant);
+}
+
 // the Gram-only path runs the fused K1 + Gram kernel (K12): f64 projector rows on a model with a K12 form, fusion on
 bool gram_fused(const sysid_engine* e, uint32_t flags) {
   return gram_prec(flags) == 0 && !gram_nullspace(e, flags) && e->k12_ok && e->fuse;
 }
 
-// staged (host entry point): chunks of at most `staged_chunk` samples, and (*stage_upto)(n) before the K1 of a
-// chunk ending at sample n (it orders `st` after the DMA of the inputs [0, n)); 0 / nullptr: the workspace's chunk
-// size, inputs already on the device.
+// staged (host entry point): the staged chunks' bounds (staged chunk k = samples [b[k], b[k+1])), and
+// (*stage_upto)(n) before the K1 of a chunk ending at sample n (it orders `st` after the DMA of the inputs [0, n));
+// nullptr: the workspace's chunk size, inputs already on the device.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
-                        int64_t staged_chunk = 0, const std::function<int(int64_t)>* stage_upto = nullptr,
-                        const K1Stream* kst = nullptr, bool chunk_major = false) {
+                        const std::vector<int64_t>* staged = nullptr,
+                        const std::function<int(int64_t)>* stage_upto = nullptr, const K1Stream* kst = nullptr,
+                        bool chunk_major = false) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
-  if (chunk_major && (staged_chunk <= 0 || gram_fused(e, flags)))
+  if (chunk_major && (!staged || gram_fused(e, flags)))
     return set_err(e, SYSID_E_INVALID, "chunk-major inputs need the staged, unfused chunk loop");
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
@@ -574,14 +581,19 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     if (ev && k < ev->size()) HIP_TRY(e, hipEventRecord((*ev)[k++], st));
     return SYSID_OK;
   };
-  const int64_t step = staged_chunk > 0 && staged_chunk < C ? staged_chunk : C;
+  size_t sc = 0;  // the staged chunk holding c0
   for (int64_t c0 = 0, n = 0; c0 < N; c0 += n) {
-    n = std::min(step, N - c0);
-    // chunk-major inputs: staged chunk k = [k0, k1) is its own (rows x (k1 - k0)) block at offset rows·k0; a
-    // launch never straddles two of them (a staged chunk larger than the workspace chunk runs as several)
-    const int64_t k0 = chunk_major ? c0 / staged_chunk * staged_chunk : 0;
-    const int64_t k1 = chunk_major ? std::min(k0 + staged_chunk, N) : N;
-    if (chunk_major) n = std::min(n, k1 - c0);
+    n = std::min(C, N - c0);
+    // staged chunk [k0, k1) (chunk-major: its own (rows x (k1 - k0)) block at offset rows·k0): a launch never
+    // straddles two of them, so each chunk's kernels wait only for its own DMA (a staged chunk larger than the
+    // workspace chunk runs as several launches)
+    int64_t k0 = 0, k1 = N;
+    if (staged) {
+      while (sc + 2 < staged->size() && (*staged)[sc + 1] <= c0) ++sc;
+      k0 = (*staged)[sc];
+      k1 = (*staged)[sc + 1];
+      n = std::min(n, k1 - c0);
+    }
     if (stage_upto && (rc = (*stage_upto)(c0 + n))) return rc;  // this chunk's inputs
     if ((rc = mark())) return rc;
     const double* cin = chunk_major ? d_in + (int64_t)e->in_rows * k0 + (c0 - k0) : d_in + c0;
@@ -676,14 +688,16 @@ class Stager {
  public:
   Stager(sysid_engine* e, int64_t N, double* d_dst) : e_(e), N_(N), d_dst_(d_dst) {}
   ~Stager() { finish(); }
-  int64_t chunk() const { return CH_; }
+  int64_t chunk() const { return CH_; }                       // streamed: the part length
+  const std::vector<int64_t>& bounds() const { return b_; }  // staged chunk c = samples [b_[c], b_[c + 1])
   bool chunk_major() const { return cm_; }
   int chunks() const { return nch_; }
   // chunk_major (the Gram-only path, one K1 launch per chunk): chunk c is packed as its own (rows x n) block at
   // offset rows·c0 of the staging block and of the device block, so it leaves as ONE contiguous DMA, and chunk c's
   // K1 reads it with ld = n (chunk_input()).  Otherwise the block keeps the caller's row-major layout (ld = N) and
   // each chunk is a 2-D DMA of one row piece per channel.
-  int begin(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, bool chunk_major = false) {
+  int begin(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, bool chunk_major = false,
+            const std::vector<int64_t>* bounds = nullptr) {
     sysid_engine* e = e_;
     cm_ = chunk_major;
     const size_t need = (size_t)e->in_rows * N_ * sizeof(double);
@@ -706,6 +720,14 @@ class Stager {
     if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
     CH_ = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
     nch_ = (int)((N_ + CH_ - 1) / CH_);
+    b_.clear();
+    if (bounds && !std::getenv("SYSID_STAGE_CHUNKS")) {
+      b_ = *bounds;
+    } else {
+      for (int c = 0; c < nch_; ++c) b_.push_back((int64_t)c * CH_);
+      b_.push_back(N_);
+    }
+    nch_ = (int)b_.size() - 1;
     if (int rc = ensure_copy_stream(e)) return rc;
     while ((int)e->stage_ev.size() < nch_) {
       hipEvent_t x;
@@ -718,7 +740,7 @@ class Stager {
     double* hs = e->h_stage;
     e->pool->start([this, T, R, hs](int t) {
       for (int c = 0; c < nch_; ++c) {
-        const int64_t c0 = c * CH_, n = std::min(CH_, N_ - c0);
+        const int64_t c0 = b_[c], n = b_[c + 1] - c0;
         for (int r = t; r < R; r += T)
           std::memcpy(cm_ ? hs + (int64_t)R * c0 + (int64_t)r * n : hs + (int64_t)r * N_ + c0, row_src_[r] + c0,
                       (size_t)n * sizeof(double));
@@ -734,7 +756,7 @@ class Stager {
     const int T = e->pool->size();
     while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
     stamp();  // SYSID_TRACE_HOST: chunk c packed
-    const int64_t c0 = c * CH_, n = std::min(CH_, N_ - c0);
+    const int64_t c0 = b_[c], n = b_[c + 1] - c0;
     const double* hs = e->h_stage;
     const int64_t R = (int64_t)row_src_.size();
     const hipError_t cr =
@@ -865,6 +887,7 @@ class Stager {
   sysid_engine* e_;
   int64_t N_, CH_ = 0;
   int nch_ = 0;
+  std::vector<int64_t> b_;  // staged chunk bounds (begin())
   double* d_dst_;
   std::vector<const double*> row_src_;  // channel row r of the block <- its source row
   std::unique_ptr<std::atomic<int>[]> done_;
@@ -1594,6 +1617,19 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     return v && std::strcmp(v, "rows") == 0;
   }();
   const bool chunk_major = staged && gram_only && !streamed && !gram_fused(e, flags) && !rows_layout;
+  // Gram-only staged chunks on K1's round boundaries: a first chunk of one round of K1 (every resident wave one step:
+  // its DMA is short, so the kernels start early), then the rest in two chunks of whole rounds, so the chunks add no
+  // partial K1 rounds to the unchunked launch's (SYSID_STAGE_CHUNKS=k: k equal chunks instead)
+  std::vector<int64_t> round_bounds;
+  if (staged && gram_only && !streamed) {
+    const int64_t R = k1_round_samples(e, gp, gram_nullspace(e, flags));
+    if (R > 0 && N >= 3 * R) {
+      const int64_t mid = R + ((N - R + 2 * R - 1) / (2 * R)) * R;  // whole rounds, the larger half first
+      round_bounds = {0, R, std::min(mid, N - 1), N};
+    } else {
+      round_bounds = {0, (N + 1) / 2, N};
+    }
+  }
   int rc;
   if (streamed) {  // the part-major device block, uncached (grow-only)
     const int64_t PL = Stager::part_len(N, e->stream_parts);
@@ -1630,7 +1666,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   if (trace) stager.trace_from(t0);
   int nstaged = 0;  // chunks sent so far
   const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
-    for (; nstaged < stager.chunks() && (int64_t)nstaged * stager.chunk() < upto; ++nstaged) {
+    for (; nstaged < stager.chunks() && stager.bounds()[nstaged] < upto; ++nstaged) {
       const int r = stager.stage(nstaged, st);
       if (r != SYSID_OK) return r;
     }
@@ -1648,7 +1684,8 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     epoch = e->in_epoch;
     __atomic_store_n(e->h_ready + K1_STREAM_ERR, 0u, __ATOMIC_SEQ_CST);
     if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, e->stream_parts)) != SYSID_OK) return fail(rc);
-  } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major)) != SYSID_OK) {
+  } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major, gram_only ? &round_bounds : nullptr)) !=
+                            SYSID_OK) {
     return fail(rc);
   }
   // the stacked-output path reads every sample in one launch: all chunks first
@@ -1672,7 +1709,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   rc = streamed  ? launch_gram_chunked(e, e->d_in_uc, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, 0,
                                        nullptr, &kst)
        : gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
-                                       staged ? stager.chunk() : 0, staged ? &stage_upto : nullptr, nullptr,
+                                       staged ? &stager.bounds() : nullptr, staged ? &stage_upto : nullptr, nullptr,
                                        chunk_major)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
   if (streamed) {  // the parts go out after the kernels are queued, and every flag is written (K1 must drain)

@@ -328,14 +328,20 @@ def test_gram_only_chunked(robot, N):
 
 
 @pytest.mark.parametrize("robot,N,chunks,ws_chunk", [("spot", 20001, 3, 0), ("spot", 4999, 2, 0), ("g1_29dof", 3001, 4, 0),
-                                                    ("spot", 20001, 2, 8 << 20), ("g1_29dof", 3001, 2, 16 << 20)])
+                                                    ("spot", 20001, 2, 8 << 20), ("g1_29dof", 3001, 2, 16 << 20),
+                                                    ("spot", 20001, 0, 0), ("spot", 40000, 0, 64 << 20),
+                                                    ("g1_29dof", 9001, 0, 0)])
 def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
     """Host Gram-only entry point with its inputs staged in `chunks` chunk-major blocks (each chunk packed as its
     own block and sent as one DMA, its K1 reading it with ld = the chunk's length), ragged last chunk, and staged
     chunks larger than the workspace's panel chunk (ws_chunk bytes: several K1 launches per staged block): the same
-    normal equations as the device entry point on the row-major block, to rounding."""
+    normal equations as the device entry point on the row-major block, to rounding.  chunks = 0: the default bounds
+    (a first chunk of one K1 round, then two chunks of whole rounds)."""
     import torch
-    monkeypatch.setenv("SYSID_STAGE_CHUNKS", str(chunks))
+    if chunks:
+        monkeypatch.setenv("SYSID_STAGE_CHUNKS", str(chunks))
+    else:
+        monkeypatch.delenv("SYSID_STAGE_CHUNKS", raising=False)
     model = load_robot(robot)
     e = Engine(model)
     if ws_chunk:
