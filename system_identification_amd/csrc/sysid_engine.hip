@@ -1620,12 +1620,19 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   // Gram-only staged chunks on K1's round boundaries: a first chunk of one round of K1 (every resident wave one step:
   // its DMA is short, so the kernels start early), then the rest in two chunks of whole rounds, so the chunks add no
   // partial K1 rounds to the unchunked launch's (SYSID_STAGE_CHUNKS=k: k equal chunks instead)
+  // (SYSID_STAGE_SPLIT=2: the one-round chunk, then the rest in one chunk)
   std::vector<int64_t> round_bounds;
   if (staged && gram_only && !streamed) {
+    static const int split = [] {
+      const char* v = std::getenv("SYSID_STAGE_SPLIT");
+      return v && std::atoi(v) == 2 ? 2 : 3;
+    }();
     const int64_t R = k1_round_samples(e, gp, gram_nullspace(e, flags));
-    if (R > 0 && N >= 3 * R) {
+    if (R > 0 && N >= 3 * R && split == 3) {
       const int64_t mid = R + ((N - R + 2 * R - 1) / (2 * R)) * R;  // whole rounds, the larger half first
       round_bounds = {0, R, std::min(mid, N - 1), N};
+    } else if (R > 0 && N >= 2 * R) {
+      round_bounds = {0, R, N};
     } else {
       round_bounds = {0, (N + 1) / 2, N};
     }
