@@ -329,7 +329,8 @@ def test_gram_only_chunked(robot, N):
 
 @pytest.mark.parametrize("robot,N,chunks,ws_chunk", [("spot", 20001, 3, 0), ("spot", 4999, 2, 0), ("g1_29dof", 3001, 4, 0),
                                                     ("spot", 20001, 2, 8 << 20), ("g1_29dof", 3001, 2, 16 << 20),
-                                                    ("spot", 20001, 0, 0), ("spot", 40000, 0, 64 << 20),
+                                                    ("spot", 20001, 0, 0), ("spot", 10000, 0, 0),
+                                                    ("spot", 40000, 0, 64 << 20),
                                                     ("g1_29dof", 9001, 0, 0)])
 def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
     """Host Gram-only entry point with its inputs staged in `chunks` chunk-major blocks (each chunk packed as its
