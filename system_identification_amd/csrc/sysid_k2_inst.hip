@@ -11,7 +11,8 @@
 #endif
 
 // rows per staged chunk of the 10-tile-column narrow Gram (Spot, solo12): 24 (K2 0.1640 ms) against 16 / 32 / 40 / 48
-// (0.1662 / 0.1650 / slower / slower; profiles/r04_s8, r03_l); -D for A/B builds only
+// (0.1662 / 0.1650 / slower / slower; profiles/r04_s8, r03_l) and 20 / 28 (+0.5% / +1.2%, r04_final2); -D for A/B
+// builds only
 #ifndef SYSID_K2_KC10
 #define SYSID_K2_KC10 24
 #endif
