@@ -330,6 +330,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # Exchange check, right after the timed region and before anything else writes the Gram buffers (the steady-state
+    # re-timing, time_stages and the e2e legs build this rank's local, un-reduced Gram into them): every rank must
+    # hold the same reduced Gram in each buffer; with
+    # the one-rank test communicator the all-reduce is the identity, so each buffer must equal a fresh local
+    # build bitwise (K1-K3 are deterministic).
+    exchange_check = None
+    if comm is not None:
+        sums = torch.stack([b_["gram"].sum() for b_ in bufsets] + [b_["gram"].abs().sum() for b_ in bufsets])
+        if world > 1:
+            hi, lo = sums.clone(), sums.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            exchange_check = {"ranks_agree": bool(torch.equal(hi, lo)), "buffers": len(bufsets)}
+        else:
+            ref_g = dict(bufs, gram=torch.zeros_like(bufs["gram"]))
+            launch(stream.cuda_stream, ref_g)
+            torch.cuda.synchronize()
+            exchange_check = {"bitwise_equal_local_build": all(bool(torch.equal(b_["gram"], ref_g["gram"]))
+                                                               for b_ in bufsets), "buffers": len(bufsets)}
+        # the packed exchange carries the row count: the job's N·nv (the Solver's 1/num_rows, solver.py:190)
+        exchange_check["num_rows"] = float(xbuf[-1].item())
+        exchange_check["num_rows_ok"] = exchange_check["num_rows"] == float(total_per_step * model.nv)
+
     # Labelled side figures, all after the timed region: the steady state (250 ms of untimed steps, then the same
     # K steps re-timed; rank 0 at N = 1) and the host-entry-point legs (SURVEY §8d's end-to-end rate,
     # PCIe-inclusive).  Neither is `value`.
@@ -367,27 +390,6 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = e2e_legs(eng, data, N)
         torch.cuda.synchronize()
-
-    # Exchange check (after the timed region): every rank must hold the same reduced Gram in each buffer; with
-    # the one-rank test communicator the all-reduce is the identity, so each buffer must equal a fresh local
-    # build bitwise (K1-K3 are deterministic).
-    exchange_check = None
-    if comm is not None:
-        sums = torch.stack([b_["gram"].sum() for b_ in bufsets] + [b_["gram"].abs().sum() for b_ in bufsets])
-        if world > 1:
-            hi, lo = sums.clone(), sums.clone()
-            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-            exchange_check = {"ranks_agree": bool(torch.equal(hi, lo)), "buffers": len(bufsets)}
-        else:
-            ref_g = dict(bufs, gram=torch.zeros_like(bufs["gram"]))
-            launch(stream.cuda_stream, ref_g)
-            torch.cuda.synchronize()
-            exchange_check = {"bitwise_equal_local_build": all(bool(torch.equal(b_["gram"], ref_g["gram"]))
-                                                               for b_ in bufsets), "buffers": len(bufsets)}
-        # the packed exchange carries the row count: the job's N·nv (the Solver's 1/num_rows, solver.py:190)
-        exchange_check["num_rows"] = float(xbuf[-1].item())
-        exchange_check["num_rows_ok"] = exchange_check["num_rows"] == float(total_per_step * model.nv)
 
     nv, W = model.nv, eng.w
     in_b = (model.nq + 2 * nv + model.nj + model.n_ee) * 8

@@ -195,7 +195,7 @@ int32_t sysid_rccl_comm_destroy(void* comm);
 int32_t sysid_allreduce_gram(const sysid_engine* e, double* d_gram, void* comm, void* stream);
 const char* sysid_rccl_last_error(void);
 /* The packed exchange: the upper triangle of the (W+1)x(W+1) device Gram (G, Aᵀb and bᵀb,
- * row by row) plus the rank's row count, (W+1)(W+2)/2 + 1 doubles (Spot 12,091, G1 64,981 — half the
+ * row by row) plus the rank's row count, (W+1)(W+2)/2 + 1 doubles (Spot W+1 = 155: 12,091, G1 W+1 = 359: 64,621 — half the
  * bytes of sysid_allreduce_gram), summed by one RCCL all-reduce and unpacked into both triangles of d_gram
  * (bitwise symmetric).  d_xbuf: a device buffer of sysid_exchange_bytes(e) bytes, 8-byte aligned; after the
  * call its last element holds the summed row count (num_rows of the whole job).  Stream-ordered. */

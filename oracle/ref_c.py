@@ -20,7 +20,7 @@ def _lib():
     lib.oracle_create.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     lib.oracle_destroy.argtypes = [ctypes.c_void_p]
     lib.oracle_build.restype = ctypes.c_int
-    lib.oracle_build.argtypes = [ctypes.c_void_p] + [_dp] * 5 + [ctypes.c_int64, ctypes.c_int64] + [_dp] * 7 + [ctypes.c_int]
+    lib.oracle_build.argtypes = [ctypes.c_void_p] + [_dp] * 5 + [ctypes.c_int64, ctypes.c_int64] + [_dp] * 8 + [ctypes.c_int]
     return lib
 
 
@@ -38,7 +38,9 @@ class COracle:
         if getattr(self, "h", None):
             self.lib.oracle_destroy(self.h)
 
-    def build(self, q, dq, ddq, tau, cnt, nthreads=1, gram=True, stacked=True):
+    def build(self, q, dq, ddq, tau, cnt, nthreads=1, gram=True, stacked=True, ymax=False):
+        """The stacked arrays and normal equations; ymax=True adds "Y_max", each sample's max |Y| of its
+        unprojected regressor (the per-sample scale of the Y_proj parity metric, tests/parity.py)."""
         m = self.model
         ins = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in (q, dq, ddq, tau, cnt)]
         N = ins[0].shape[1]
@@ -50,7 +52,9 @@ class COracle:
         G = np.empty((W, W)) if gram else None
         g = np.empty(W) if gram else None
         bb = np.zeros(1)
+        ym = np.empty(N) if ymax else None
         p = lambda a: a.ctypes.data_as(_dp) if a is not None else None  # noqa: E731
         self.lib.oracle_build(self.h, *[p(a) for a in ins], N, ins[0].strides[0] // 8,
-                              p(Y), p(t), p(Bv), p(Bc), p(G), p(g), p(bb), int(nthreads))
-        return {"Y_proj": Y, "tau_proj": t, "B_v": Bv, "B_c": Bc, "gram": G, "Atb": g, "btb": float(bb[0])}
+                              p(Y), p(t), p(Bv), p(Bc), p(G), p(g), p(bb), p(ym), int(nthreads))
+        return {"Y_proj": Y, "tau_proj": t, "B_v": Bv, "B_c": Bc, "gram": G, "Atb": g, "btb": float(bb[0]),
+                "Y_max": ym}

@@ -289,7 +289,7 @@ void oracle_destroy(void* o) { free(o); }
  * Bv, Bc (N nv x na), G (W x W), g (W), btb.  Any output may be NULL.  nthreads <= 0: all cores. */
 int oracle_build(void* h, const double* q, const double* dq, const double* ddq, const double* tau,
                  const double* cnt, int64_t N, int64_t ld, double* Y, double* tp, double* Bv, double* Bc,
-                 double* G, double* g, double* btb, int nthreads) {
+                 double* G, double* g, double* btb, double* ymax, int nthreads) {
   const omodel* m = &((oracle_t*)h)->m;
   const int nv = m->nv, nb = m->nj_total - 1, na = m->na, bd = m->bd, wy = 10 * nb, W = wy + 2 * na;
   if (G) memset(G, 0, sizeof(double) * W * W);
@@ -319,6 +319,11 @@ int oracle_build(void* h, const double* q, const double* dq, const double* ddq, 
       /* pass 1: get_proj_regressor_torque (src/sys_identification.py:401-410) */
       forward(m, qs, vs, as, d);
       joint_torque_regressor(m, d, Ys);
+      if (ymax) { /* the sample's unprojected scale: the floor of the per-sample Y_proj parity metric */
+        double mx = 0.0;
+        for (int x = 0; x < nv * wy; ++x) mx = fabs(Ys[x]) > mx ? fabs(Ys[x]) : mx;
+        ymax[s] = mx;
+      }
       projector(m, d, cs, P);
       for (int r = 0; r < nv; ++r) {
         for (int c = 0; c < wy; ++c) {

@@ -155,12 +155,6 @@ struct sysid_engine {
   size_t h_stage_cap = 0;
   HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
   hipStream_t copy_stream = nullptr;     // host API: the staged input chunks' DMA (created on first use)
-  unsigned* h_ready = nullptr;           // host API, streamed inputs: per-part flags + error word in coherent host
-                                         // memory (K1Params::in_ready), written by the host
-  double* d_in_uc = nullptr;             // streamed inputs: the part-major device block (uncached, grow-only)
-  size_t in_uc_cap = 0;
-  unsigned in_epoch = 0;                 // the flags' value of the current call
-  int stream_parts = 0;                  // parts per claim shard (SYSID_STREAM_PARTS; 0: no streaming)
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -271,23 +265,11 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Streamed inputs of one K1 launch (K1Params::in_ready): the host entry point's Gram-only path.
-struct K1Stream {
-  const unsigned* ready;
-  int part;
-  unsigned epoch;
-};
-
 // cmp: the Gram-only nullspace mode (rcount: its per-sample row counts).
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
               unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0, int cmp = 0,
-              int* rcount = nullptr, const K1Stream* kst = nullptr) {
+              int* rcount = nullptr) {
   K1Params kp = e->kp;
-  if (kst) {
-    kp.in_ready = kst->ready;
-    kp.in_part = kst->part;
-    kp.in_epoch = kst->epoch;
-  }
   HIP_TRY(e, zero_async(work, WORK_BYTES, st));
   if (full) {
     kp.full = 1;
@@ -303,8 +285,6 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
   kp.out_cols = (int)std::min<int64_t>(ld_panel, prec == 0 ? e->ldp : ld_panel);
   const int64_t waves_needed = (N + spw - 1) / spw;
   const int64_t cap = (int64_t)e->cus * bpc;
-  // (streamed inputs: the copies are copy-engine DMAs and the flags host stores, so a full grid never waits on
-  // a kernel that cannot become resident)
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(cap, (waves_needed + waves - 1) / waves));
   const dim3 g1((unsigned)grid), b1(64 * waves);
   // the instantiation unit of (panel type, row mode)
@@ -534,8 +514,7 @@ bool gram_fused(const sysid_engine* e, uint32_t flags) {
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
                         const std::vector<int64_t>* staged = nullptr,
-                        const std::function<int(int64_t)>* stage_upto = nullptr, const K1Stream* kst = nullptr,
-                        bool chunk_major = false) {
+                        const std::function<int(int64_t)>* stage_upto = nullptr, bool chunk_major = false) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
@@ -599,13 +578,13 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     const double* cin = chunk_major ? d_in + (int64_t)e->in_rows * k0 + (c0 - k0) : d_in + c0;
     const int64_t cld = chunk_major ? k1 - k0 : ld;
     if (cmp) {
-      if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, kst)))
+      if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount)))
         return rc;
       const unsigned nseg = (unsigned)((n + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG);
       hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
       hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, rseg, (int)n, e->nv, rowlist, d_rows);
       HIP_TRY(e, hipGetLastError());
-    } else if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr, kst))) {
+    } else if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr))) {
       return rc;
     }
     if ((rc = mark())) return rc;
@@ -668,7 +647,7 @@ int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemc
 // is reused by the next call only after this call's launch-stream synchronise, which follows every DMA.
 // The host entry points' copy stream, created on first use and warmed by one small DMA: the runtime sets up the
 // stream's copy queue lazily on its first copy, which under a resident full-chip K1 took milliseconds
-// (profiles/r04_s3: the first streamed call's first part started 8 ms after K1).
+// (profiles/r04_s3).
 int ensure_copy_stream(sysid_engine* e) {
   if (e->copy_stream) return SYSID_OK;
   HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
@@ -688,7 +667,6 @@ class Stager {
  public:
   Stager(sysid_engine* e, int64_t N, double* d_dst) : e_(e), N_(N), d_dst_(d_dst) {}
   ~Stager() { finish(); }
-  int64_t chunk() const { return CH_; }                       // streamed: the part length
   const std::vector<int64_t>& bounds() const { return b_; }  // staged chunk c = samples [b_[c], b_[c + 1])
   bool chunk_major() const { return cm_; }
   int chunks() const { return nch_; }
@@ -781,109 +759,7 @@ class Stager {
     started_ = false;
   }
 
-  // Streamed form (the Gram-only path when it is one chunk: ONE K1 launch over all N whose waves wait per part,
-  // K1Params::in_ready).  Part p is the shard-relative samples [p·PL, (p+1)·PL) of every claim shard
-  // (k1_shard_begin), so the K1 waves of every XCD start on part 0 together; it is packed part-major — piece (p,
-  // shard x) = R rows x PL samples at offset (p·K1_SHARDS + x)·R·PL — and leaves as ONE contiguous DMA.
-  // send_streamed() enqueues the parts' DMAs with an event each; flag_streamed() then writes in_ready[p] = epoch in
-  // host memory as each DMA completes.
-  static int64_t part_len(int64_t N, int parts) {
-    int64_t maxlen = 0;
-    for (int x = 0; x < K1_SHARDS; ++x) maxlen = std::max(maxlen, k1_shard_begin(N, x + 1) - k1_shard_begin(N, x));
-    parts = std::max(1, std::min(parts, K1_STREAM_ERR));
-    return std::max<int64_t>(16, ((maxlen + parts - 1) / parts + 15) / 16 * 16);  // whole 128-byte lines
-  }
-  static int part_count(int64_t N, int64_t PL) {
-    int64_t maxlen = 0;
-    for (int x = 0; x < K1_SHARDS; ++x) maxlen = std::max(maxlen, k1_shard_begin(N, x + 1) - k1_shard_begin(N, x));
-    return (int)std::max<int64_t>(1, (maxlen + PL - 1) / PL);
-  }
-  int begin_streamed(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, int parts) {
-    sysid_engine* e = e_;
-    CH_ = part_len(N_, parts);
-    nch_ = part_count(N_, CH_);
-    for (int k = 0; k < nsrc; ++k)
-      for (int r = 0; r < nrows[k]; ++r) row_src_.push_back(srcs[k] + (int64_t)r * ld);
-    const int64_t R = (int64_t)row_src_.size();
-    const size_t need = (size_t)nch_ * K1_SHARDS * R * CH_ * sizeof(double);
-    if (need > e->h_stage_cap) {
-      if (e->h_stage) (void)hipHostFree(e->h_stage);
-      e->h_stage = nullptr;
-      e->h_stage_cap = 0;
-      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
-      e->h_stage_cap = need;
-    }
-    if (!e->pool) {
-      int T = 8;
-      if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
-      e->pool = new HostPool(T);
-    }
-    if (int rc = ensure_copy_stream(e)) return rc;
-    while ((int)e->stage_ev.size() < nch_) {
-      hipEvent_t x;
-      HIP_TRY(e, hipEventCreateWithFlags(&x, hipEventDisableTiming));
-      e->stage_ev.push_back(x);
-    }
-    done_.reset(new std::atomic<int>[nch_]);
-    for (int c = 0; c < nch_; ++c) done_[c].store(0);
-    const int T = e->pool->size();
-    double* hs = e->h_stage;
-    e->pool->start([this, T, R, hs](int t) {
-      for (int c = 0; c < nch_; ++c) {
-        for (int x = 0; x < K1_SHARDS; ++x) {
-          int64_t c0, n;
-          piece(c, x, &c0, &n);
-          double* blk = hs + ((int64_t)c * K1_SHARDS + x) * R * CH_;
-          if (n > 0)
-            for (int64_t r = t; r < R; r += T)
-              std::memcpy(blk + r * CH_, row_src_[r] + c0, (size_t)n * sizeof(double));
-        }
-        done_[c].fetch_add(1, std::memory_order_release);
-      }
-    });
-    started_ = true;
-    return SYSID_OK;
-  }
-  size_t streamed_bytes() const { return (size_t)nch_ * K1_SHARDS * row_src_.size() * CH_ * sizeof(double); }
-  int send_streamed() {
-    sysid_engine* e = e_;
-    const int T = e->pool->size();
-    const size_t pb = (size_t)K1_SHARDS * row_src_.size() * CH_;  // doubles per part
-    for (int c = 0; c < nch_; ++c) {
-      while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
-      stamp();
-      if (hipMemcpyAsync(d_dst_ + c * pb, e->h_stage + c * pb, pb * sizeof(double), hipMemcpyHostToDevice,
-                         e->copy_stream) != hipSuccess ||
-          hipEventRecord(e->stage_ev[c], e->copy_stream) != hipSuccess)
-        return set_err(e, SYSID_E_DEVICE, "input copy failed");
-    }
-    return SYSID_OK;
-  }
-  // in_ready[c] = epoch as part c's DMA completes (every flag is written, also after an error, so K1 drains)
-  // (bounded: a DMA not done 2 s after the call began is reported, and its flag written anyway so K1 drains)
-  int flag_streamed(unsigned* h_ready, unsigned epoch) {
-    int rc = SYSID_OK;
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(2);
-    for (int c = 0; c < nch_; ++c) {
-      hipError_t q;
-      while ((q = hipEventQuery(e_->stage_ev[c])) == hipErrorNotReady && std::chrono::steady_clock::now() < deadline)
-        std::this_thread::yield();
-      if (q != hipSuccess && rc == SYSID_OK)
-        rc = set_err(e_, SYSID_E_DEVICE, "streamed inputs: part %d of %d: %s", c, nch_,
-                     q == hipErrorNotReady ? "its DMA had not completed after 2 s" : hipGetErrorString(q));
-      __atomic_store_n(h_ready + c, epoch, __ATOMIC_SEQ_CST);
-      stamp();
-    }
-    return rc;
-  }
-
  private:
-  void piece(int c, int x, int64_t* c0, int64_t* n) const {  // part c of shard x
-    const int64_t b = k1_shard_begin(N_, x), en = k1_shard_begin(N_, x + 1);
-    *c0 = b + c * CH_;
-    *n = std::max<int64_t>(0, std::min(en, *c0 + CH_) - *c0);
-  }
-
   sysid_engine* e_;
   int64_t N_, CH_ = 0;
   int nch_ = 0;
@@ -1214,7 +1090,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
-  if (const char* v = std::getenv("SYSID_STREAM_PARTS")) e->stream_parts = std::max(0, std::atoi(v));
   if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   for (int p = 0; p < 3; ++p) {
@@ -1314,8 +1189,6 @@ void sysid_destroy(sysid_engine* e) {
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   delete e->pool;
   for (hipEvent_t x : e->stage_ev) (void)hipEventDestroy(x);
-  if (e->h_ready) (void)hipHostFree(e->h_ready);
-  if (e->d_in_uc) (void)hipFree(e->d_in_uc);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -1606,23 +1479,20 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
                          ((flags & SYSID_EMIT_FRICTION) && (B_v || B_c) && e->nj);
   const bool gram_only = want_gram && !panel_out;
   const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
-  // streamed (Gram-only, one chunk, unfused): one K1 launch consumes the inputs as their parts land
   const int gp = gram_prec(flags);
-  const bool streamed = staged && gram_only && e->stream_parts > 0 && N <= gram_chunk(e, N, gp) &&
-                        !gram_fused(e, flags);
   // Gram-only, chunk by chunk: each chunk packed as its own block and sent as one contiguous DMA
   // (SYSID_STAGE_LAYOUT=rows: the row-major block, a 2-D DMA per chunk)
   static const bool rows_layout = [] {
     const char* v = std::getenv("SYSID_STAGE_LAYOUT");
     return v && std::strcmp(v, "rows") == 0;
   }();
-  const bool chunk_major = staged && gram_only && !streamed && !gram_fused(e, flags) && !rows_layout;
+  const bool chunk_major = staged && gram_only && !gram_fused(e, flags) && !rows_layout;
   // Gram-only staged chunks on K1's round boundaries: a first chunk of one round of K1 (every resident wave one step:
   // its DMA is short, so the kernels start early), then the rest in two chunks of whole rounds, so the chunks add no
   // partial K1 rounds to the unchunked launch's (SYSID_STAGE_CHUNKS=k: k equal chunks instead)
   // (SYSID_STAGE_SPLIT=2: the one-round chunk, then the rest in one chunk)
   std::vector<int64_t> round_bounds;
-  if (staged && gram_only && !streamed) {
+  if (staged && gram_only) {
     static const int split = [] {
       const char* v = std::getenv("SYSID_STAGE_SPLIT");
       return v && std::atoi(v) == 2 ? 2 : 3;
@@ -1638,17 +1508,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
   }
   int rc;
-  if (streamed) {  // the part-major device block, uncached (grow-only)
-    const int64_t PL = Stager::part_len(N, e->stream_parts);
-    const size_t need = (size_t)Stager::part_count(N, PL) * K1_SHARDS * e->in_rows * PL * sizeof(double);
-    if (need > e->in_uc_cap) {
-      if (e->d_in_uc) (void)hipFree(e->d_in_uc);
-      e->d_in_uc = nullptr;
-      e->in_uc_cap = 0;
-      HIP_TRY(e, hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_in_uc), need, hipDeviceMallocUncached));
-      e->in_uc_cap = need;
-    }
-  } else if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) {
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) {
     return rc;
   }
   if (!gram_only &&
@@ -1669,7 +1529,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   // host threads for blocks of 1 MiB and more (stage_inputs), else one copy per array
   const double* srcs[5] = {q, dq, ddq, tau, cnt};
   const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
-  Stager stager(e, N, streamed ? e->d_in_uc : e->d_in);
+  Stager stager(e, N, e->d_in);
   if (trace) stager.trace_from(t0);
   int nstaged = 0;  // chunks sent so far
   const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
@@ -1679,19 +1539,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     return SYSID_OK;
   };
-  unsigned epoch = 0;
-  if (streamed) {
-    if (!e->h_ready) {
-      // coherent host memory: the host's stores reach K1's system-scope polling loads while K1 runs
-      HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_ready), (K1_STREAM_ERR + 1) * sizeof(unsigned),
-                               hipHostMallocCoherent));
-      std::memset(e->h_ready, 0, (K1_STREAM_ERR + 1) * sizeof(unsigned));
-    }
-    if (++e->in_epoch == 0) ++e->in_epoch;  // never 0, the flags' initial value
-    epoch = e->in_epoch;
-    __atomic_store_n(e->h_ready + K1_STREAM_ERR, 0u, __ATOMIC_SEQ_CST);
-    if ((rc = stager.begin_streamed(srcs, nrows, 5, ld, e->stream_parts)) != SYSID_OK) return fail(rc);
-  } else if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major, gram_only ? &round_bounds : nullptr)) !=
+  if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major, gram_only ? &round_bounds : nullptr)) !=
                             SYSID_OK) {
     return fail(rc);
   }
@@ -1712,19 +1560,9 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     }
     r0 += nrows[k];
   }
-  const K1Stream kst{e->h_ready, (int)stager.chunk(), epoch};
-  rc = streamed  ? launch_gram_chunked(e, e->d_in_uc, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr, 0,
-                                       nullptr, &kst)
-       : gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
-                                       staged ? &stager.bounds() : nullptr, staged ? &stage_upto : nullptr, nullptr,
-                                       chunk_major)
+  rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
+                                       staged ? &stager.bounds() : nullptr, staged ? &stage_upto : nullptr, chunk_major)
                  : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
-  if (streamed) {  // the parts go out after the kernels are queued, and every flag is written (K1 must drain)
-    const int rs = stager.send_streamed();
-    if (rc == SYSID_OK) rc = rs;
-    const int rf = stager.flag_streamed(e->h_ready, epoch);
-    if (rc == SYSID_OK) rc = rf;
-  }
   if (rc != SYSID_OK) return fail(rc);
   const double t_kern = ms_since(t0);  // + kernels enqueued (before the output copies)
   if (panel_out) {
@@ -1762,11 +1600,6 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const hipError_t sst = hipStreamSynchronize(st);
   host_unregister(e, reg);
   tph[3] = ms_since(t0);  // + synchronised
-  if (sst == hipSuccess && streamed && __atomic_load_n(e->h_ready + K1_STREAM_ERR, __ATOMIC_SEQ_CST)) {
-    const unsigned* fl = e->h_ready;
-    return set_err(e, SYSID_E_DEVICE, "streamed inputs: a K1 wave gave up waiting for its part (epoch %u, flags %u %u %u %u)",
-                   epoch, fl[0], fl[1], fl[2], fl[3]);
-  }
   if (trace)
     std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, kernels enqueued "
                  "%.3f, launched %.3f, done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], t_kern, tph[2],
@@ -1885,6 +1718,8 @@ size_t sysid_exchange_bytes(const sysid_engine* e) {
 // sysid_rccl.cpp's hooks (one library, so the RCCL translation unit stays free of device code)
 int32_t sysid_internal_xchg_pack(const sysid_engine* e, const double* d_gram, double rows, double* d_x, void* stream) {
   const int n = e->ncol;
+  // a NULL stream is the null stream of the CURRENT device: make that the engine's (the unpack follows on it)
+  if (hipSetDevice(e->device) != hipSuccess) return SYSID_E_DEVICE;
   hipLaunchKernelGGL(xchg_pack, dim3((unsigned)(((int64_t)n * n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), d_gram, n, rows, d_x);
   return hipGetLastError() == hipSuccess ? SYSID_OK : SYSID_E_DEVICE;

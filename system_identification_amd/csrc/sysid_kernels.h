@@ -156,21 +156,11 @@ struct K1Params {
   int pov;          // 1: P overlays the projector's working set (wave_layout `pov`)
   double thr_rel;   // rank cut of the projector: remaining row norm <= thr_rel * the largest row norm
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
-  // Streamed inputs (the host entry point's Gram-only path, null otherwise): the input block arrives during the
-  // launch in part-major order — part p = the shard-relative samples [p·in_part, (p+1)·in_part) of every claim
-  // shard, one DMA — and part p is flagged by in_ready[p] reaching in_epoch.  in_ready lives in coherent host
-  // memory and is written by the host once the part's DMA has completed (a copy engine's or blit kernel's flag
-  // write on another stream does not progress while a full-chip kernel spins: profiles/r04_s3); in_ready[K1_STREAM_ERR]
-  // is set when a wait gives up.
-  const unsigned* in_ready;
-  int in_part;
-  unsigned in_epoch;
 };
 constexpr int K1_QUAD_IN_MAX = 96;  // input channels of the quadruped K1 (nv = 18, two samples per wave)
-constexpr int K1_STREAM_ERR = 64;  // in_ready slot of the streamed-input error word (parts < 64)
 
 // Start of claim shard x of N samples: multiples of 16 samples (one 128-byte line of a channel row), so with a
-// 16-sample-aligned row pitch no line of the input block spans two shards or two streamed parts.
+// 16-sample-aligned row pitch no line of the input block spans two shards.
 __host__ __device__ inline int64_t k1_shard_begin(int64_t N, int x) {
   return x >= K1_SHARDS ? N : (N * x / K1_SHARDS) / 16 * 16;
 }
@@ -641,34 +631,8 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   for (int u = 0; u < NXR; ++u) xr[u] = 0.0;
   auto fetch = [&](int64_t s) {  // s = the step's first sample; this half's is s + half
     const int64_t sh = s + half;
-    // channel c of the sample at in[ib + c·is]: the row-major block (ib = sh, is = ld) or, streamed, the sample's
-    // column of its (part, shard) piece of the part-major block (is = in_part)
-    int64_t ib = sh, is = ld;
-    if constexpr (!FUSED) {
-      if (kp.in_ready != nullptr && sh < N) {
-        // streamed inputs: wait until this sample's part has landed (its shard, then the part within it).  The
-        // flag is read at system scope (host memory written by the host); the input loads below issue after the
-        // loop exits, from an uncached device block (no L2 line of an earlier call's inputs can be hit).
-        int x = (int)(sh * K1_SHARDS / N);
-        while (x > 0 && k1_shard_begin(N, x) > sh) --x;
-        while (x + 1 < K1_SHARDS && k1_shard_begin(N, x + 1) <= sh) ++x;
-        const int64_t so = sh - k1_shard_begin(N, x);
-        const int part = (int)(so / kp.in_part);
-        // part-major block: (part, shard) pieces of IN rows x in_part samples each, one DMA per part
-        ib = ((int64_t)(part * K1_SHARDS + x) * IN) * kp.in_part + (so - (int64_t)part * kp.in_part);
-        is = kp.in_part;
-        const uint64_t t_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-        while ((int)(__hip_atomic_load(kp.in_ready + part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - kp.in_epoch) < 0) {
-          __builtin_amdgcn_s_sleep(4);
-          if (__builtin_amdgcn_s_memrealtime() - t_start > 100000000ull) {  // 1 s: report instead of hanging the device
-            __hip_atomic_store(const_cast<unsigned*>(kp.in_ready) + K1_STREAM_ERR, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-          }
-        }
-        asm volatile("" ::: "memory");
-      }
-    }
+    // channel c of the sample at in[ib + c·is] (the row-major block: ib = sh, is = ld)
+    const int64_t ib = sh, is = ld;
 #pragma unroll
     for (int u = 0; u < NXR; ++u)
       if (hl + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hl + HW * u) * is + ib];

@@ -50,7 +50,7 @@ def unpack_normal_equations(buf, num_rows: int) -> dict:
 def pack_upper(buf, rows) -> np.ndarray:
     """The exchange format of SURVEY.md §8e (and of the device's sysid_allreduce_normal_equations): the upper
     triangle of the n x n buffer row by row (row i at i n - i (i - 1) / 2), then the row count: n (n + 1) / 2 + 1
-    doubles (Spot 12,091, G1 64,981)."""
+    doubles (Spot n = W+1 = 155: 12,091; G1 n = 359: 64,621)."""
     buf = np.asarray(buf, dtype=np.float64)
     n = buf.shape[0]
     return np.concatenate([buf[np.triu_indices(n)], [float(rows)]])
@@ -119,10 +119,21 @@ class RcclGramComm:
         if self.lib.sysid_rccl_comm_init(ctypes.byref(self._comm), int(world), uid, int(rank), int(engine.device)) != 0:
             raise RuntimeError(self.lib.sysid_rccl_last_error().decode())
 
+    def _check(self, t, n: int, what: str):
+        """The C side trusts the buffer sizes: a float64 tensor of exactly n elements on the engine's device."""
+        import torch
+        if (not isinstance(t, torch.Tensor) or t.dtype != torch.float64 or t.device.type != "cuda"
+                or t.device.index != self.engine.device or t.numel() != n or not t.is_contiguous()):
+            raise ValueError(f"{what}: need a contiguous float64 tensor of {n} elements on cuda:{self.engine.device}, "
+                             f"got {getattr(t, 'dtype', type(t))} {tuple(getattr(t, 'shape', ()))} on "
+                             f"{getattr(t, 'device', None)}")
+
     def allreduce_gram(self, gram, stream=None):
         """In-place sum of a (W+1)x(W+1) float64 CUDA tensor over the ranks (stream-ordered)."""
         import ctypes
         import torch
+        n = self.engine.w + 1
+        self._check(gram, n * n, "gram")
         st = stream if stream is not None else torch.cuda.current_stream(self.engine.device).cuda_stream
         if self.lib.sysid_allreduce_gram(self.engine._h, ctypes.c_void_p(gram.data_ptr()), self._comm,
                                          ctypes.c_void_p(st)) != 0:
@@ -140,6 +151,9 @@ class RcclGramComm:
         xbuf[-1] holds the job's row count.  Stream-ordered."""
         import ctypes
         import torch
+        n = self.engine.w + 1
+        self._check(gram, n * n, "gram")
+        self._check(xbuf, int(self.lib.sysid_exchange_bytes(self.engine._h)) // 8, "xbuf")
         st = stream if stream is not None else torch.cuda.current_stream(self.engine.device).cuda_stream
         if self.lib.sysid_allreduce_normal_equations(self.engine._h, ctypes.c_void_p(gram.data_ptr()),
                                                       ctypes.c_void_p(xbuf.data_ptr()), float(rows), self._comm,

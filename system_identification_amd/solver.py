@@ -87,10 +87,12 @@ class Solver():
 
     # ------------ Constrained Solver (LMI) ------------ #
     def solve_fully_consistent(self, lambda_reg=1e-1, tol=1e-10, max_iters=1000, reg_type="constant_pullback"):
-        """solver.py:123-210.  ``reg_type`` is one of REG_TYPES; an unknown name raises ValueError (the reference
-        silently solves without a regulariser there, solver.py:161-180)."""
+        """solver.py:123-210.  ``reg_type`` is one of REG_TYPES.  Any other name solves without a regulariser, as the
+        reference does (its if / elif chain, solver.py:161-180, adds nothing for it); this mirror also warns."""
         if reg_type not in REG_TYPES:
-            raise ValueError(f"unknown reg_type {reg_type!r}: expected one of {REG_TYPES}")
+            import warnings
+            warnings.warn(f"unknown reg_type {reg_type!r} (expected one of {REG_TYPES}): solving without a "
+                          "regulariser, as src/solver.py does", RuntimeWarning, stacklevel=2)
         try:
             import cvxpy as cp  # noqa: F401
         except ImportError as exc:  # pragma: no cover - depends on the host image
@@ -119,13 +121,19 @@ def spatial_body_inertia_matrix(phi):
 
 
 def pseudo_inertia_matrix(phi):
-    """solver.py:53-63 — J (4x4): [[tr/2 - I_xx, -I_xy, -I_xz, h_x], ..., [h_x, h_y, h_z, m]], tr = I_xx+I_yy+I_zz."""
-    m, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = np.asarray(phi, dtype=np.float64)
-    tr = 0.5 * (Ixx + Iyy + Izz)
+    """solver.py:53-63 — J (4x4): [[tr/2 - I_xx, -I_xy, -I_xz, h_x], ..., [h_x, h_y, h_z, m]], tr = I_xx+I_yy+I_zz.
+    The entries are formed in phi's own dtype, as the reference's unpacking of a numpy slice does: the prior is
+    float32 (src/sys_identification.py:61), so its trace and diagonal are float32 sums (numpy 2 keeps the Python
+    scalar 1/2 weak), and only the finished matrix is float64 (cvxpy's `.value`)."""
+    phi = np.asarray(phi)
+    if phi.dtype not in (np.float32, np.float64):
+        phi = phi.astype(np.float64)
+    m, hx, hy, hz, Ixx, Ixy, Ixz, Iyy, Iyz, Izz = phi
+    tr = (1 / 2) * (Ixx + Iyy + Izz)
     return np.array([[tr - Ixx, -Ixy, -Ixz, hx],
                      [-Ixy, tr - Iyy, -Iyz, hy],
                      [-Ixz, -Iyz, tr - Izz, hz],
-                     [hx, hy, hz, m]])
+                     [hx, hy, hz, m]], dtype=np.float64)
 
 
 def ellipsoid_matrix(semi_axes, center):
@@ -243,7 +251,10 @@ def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_typ
     for idx in range(s._num_links):
         j = idx * s._num_inertial_params
         p = phi[j:j + s._num_inertial_params]
-        prior = np.asarray(s._phi_prior[j:j + s._num_inertial_params], dtype=float)
+        # the prior slice keeps its dtype (float32 from get_phi_prior) for the metric and the entropic constants,
+        # whose pseudo-inertia sums the reference forms in that dtype; as a cvxpy constant it is exact in float64
+        prior_raw = np.asarray(s._phi_prior[j:j + s._num_inertial_params])
+        prior = prior_raw.astype(np.float64)
         ell = s._bounding_ellipsoids[idx]
         semi, center = np.asarray(ell["semi_axes"]), np.asarray(ell["center"])
         cons.append(p[0] >= 0)
@@ -254,10 +265,10 @@ def _solve_fully_consistent_cvxpy(s: Solver, lambda_reg, tol, max_iters, reg_typ
         cons.append(com + eps * cp.Constant(np.eye(4)) >> 0)
         cons.append(cp.trace(J @ ellipsoid_matrix(semi, center)) >= 0)
         if reg_type == "constant_pullback":
-            reg += 0.5 * cp.quad_form(p - prior, pullback_metric(prior))
+            reg += 0.5 * cp.quad_form(p - prior, pullback_metric(prior_raw))
         elif reg_type == "entropic":
             # solver.py:164-172 (the reference notes that this form may not converge)
-            X_map, log_det_prior = entropic_prior_terms(prior)
+            X_map, log_det_prior = entropic_prior_terms(prior_raw)
             reg += -cp.log_det(J) + log_det_prior + cp.trace(X_map @ J) - 4
     if reg_type == "euclidean":
         reg = cp.quad_form(phi - np.asarray(s._phi_prior, dtype=float), np.eye(nx))

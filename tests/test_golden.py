@@ -36,10 +36,13 @@ def test_numpy_oracle_reproduces_golden(robot):
 def test_c_oracle_matches_golden(robot):
     from oracle.ref_c import COracle
     g, m = load(robot), load_robot(robot)
-    o = COracle(m).build(g["q"], g["dq"], g["ddq"], g["tau"], g["contact"], nthreads=2)
+    o = COracle(m).build(g["q"], g["dq"], g["ddq"], g["tau"], g["contact"], nthreads=2, ymax=True)
     for k in ("Y_proj", "tau_proj", "B_v", "B_c", "gram", "Atb"):
         assert rel(o[k], g[k]) < 1e-10, k
     assert abs(o["btb"] - float(g["btb"])) <= 1e-10 * abs(float(g["btb"]))
+    # the per-sample unprojected scale the whole-N Y_proj metric floors with (tests/test_gpu_full_n.py)
+    want = [sc[0] for sc in unprojected_scales(m, g["q"], g["dq"], g["ddq"], g["tau"])]
+    assert np.allclose(o["Y_max"], want, rtol=1e-12, atol=0)
 
 
 @pytest.mark.parametrize("robot", ROBOTS)

@@ -2,14 +2,14 @@
 stacked panel and the whole Gram / Aᵀb / bᵀb against the C oracle (oracle/sysid_oracle.c, OpenMP on the box's
 16 threads) at north_star's 1e-6 — not sampled subsets.
 
-* config 1 Solo-12 2k, config 2 Spot 20k (the headline workload, fused K1 + Gram) and config 3 G1 20k: the whole
-  panel, per sample block, and the whole normal equations;
+* config 1 Solo-12 2k, config 2 Spot 20k (the headline workload) and config 3 G1 20k: the whole panel, per sample
+  block, and the whole normal equations;
 * config 4 Spot 200k and config 5 G1 1M (f64 Gram-only): the whole normal equations (tests/test_gpu_configs.py
   holds their shard-sum and sampled-panel checks).
-Per-block metric: max |a - b| over the block / max(max |b| over the block, 1e-4 x a scale): the sample's |tau|
-for tau_proj, its joint |dq| for B_v, 1 for B_c, and the whole stacked Y_proj's max for Y_proj (the sampled tests
-use each sample's unprojected regressor; a whole-N pass has no cheap unprojected Y, and the floor binds only for
-blocks 1e4 below the largest).  Run times are printed (pytest -s) and listed by --durations (tests/conftest.py).
+Per-block metric: max |a - b| over the block / max(max |b| over the block, 1e-4 x the sample's unprojected scale):
+its |tau| for tau_proj, its joint |dq| for B_v, 1 for B_c, and its unprojected regressor's max |Y| for Y_proj (the
+C oracle reports it per sample, oracle_build's ymax), as the sampled tests do (tests/parity.py).  Run times are
+printed (pytest -s) and listed by --durations (tests/conftest.py).
 Reference: demo/spot_identification.py:84-87, src/solver.py:186-190."""
 import time
 
@@ -60,14 +60,14 @@ def test_whole_panel_and_gram_vs_oracle(robot, N, cfg):
     P = bufs["panel"][: N * model.nv].cpu().numpy()
     G = bufs["gram"].cpu().numpy()
     t0 = time.perf_counter()
-    o = COracle(model).build(*[d[k] for k in CH], nthreads=16)
+    o = COracle(model).build(*[d[k] for k in CH], nthreads=16, ymax=True)
     t_o = time.perf_counter() - t0
     nv, wy, nj, W = model.nv, e.wy, e.nj, e.w
     bd = model.base_dof
     tau_s = np.abs(d["tau"]).max(axis=0)
     dq_s = np.abs(d["dq"][bd:]).max(axis=0)
     errs = {
-        "Y_proj": block_errors(P[:, :wy], o["Y_proj"], N, nv, FLOOR * np.abs(o["Y_proj"]).max()),
+        "Y_proj": block_errors(P[:, :wy], o["Y_proj"], N, nv, FLOOR * o["Y_max"]),
         "tau_proj": block_errors(P[:, W], o["tau_proj"], N, nv, FLOOR * tau_s),
         "B_v": block_errors(P[:, wy:wy + nj], o["B_v"], N, nv, FLOOR * dq_s),
         "B_c": block_errors(P[:, wy + nj:W], o["B_c"], N, nv, FLOOR),

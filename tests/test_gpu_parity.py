@@ -361,35 +361,6 @@ def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
     assert only["num_rows"] == N * model.nv
 
 
-@pytest.mark.parametrize("robot,N,parts", [("spot", 20000, 2), ("spot", 9999, 4)])
-def test_host_gram_only_streamed_inputs(robot, N, parts, monkeypatch):
-    """Streamed inputs (SYSID_STREAM_PARTS, opt-in): one K1 launch whose waves wait per part for host-written flags
-    while the parts' DMAs land in an uncached part-major block.  Three calls on one engine with different inputs (A,
-    B, A: a wave reading a stale line of the previous call's inputs would show), each against the device entry
-    point on the row-major block.  (G1 is not covered: under its resident K1 the parts' DMAs ran hundreds of
-    microseconds apart and a wave's 1 s wait expired, reported as an error — profiles/r04_s5.)"""
-    import torch
-    monkeypatch.setenv("SYSID_STREAM_PARTS", str(parts))
-    model = load_robot(robot)
-    e = Engine(model)
-    ref_e = eng(robot)
-    W = ref_e.w
-    data = [generate(model, N, config_index=c) for c in (5, 6)]
-    refs = []
-    for d in data:
-        din = torch.from_numpy(channel_block(d)).cuda()
-        bufs = ref_e.alloc_gram_device(N)
-        ref_e.build_gram_device(din, N, bufs)
-        torch.cuda.synchronize()
-        refs.append(bufs["gram"].cpu().numpy())
-    for k in (0, 1, 0):
-        d, G = data[k], refs[k]
-        out = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_GRAM)
-        assert rel(out["gram"], G[:W, :W]) < 1e-12, k
-        assert rel(out["Atb"], G[:W, W]) < 1e-12, k
-        assert abs(out["btb"] - G[W, W]) <= 1e-12 * abs(G[W, W]), k
-
-
 @pytest.mark.parametrize("robot,N", [("spot", 3000), ("g1_29dof", 700)])
 def test_tau_prediction_rmse_reduction(robot, N):
     """K4 (device reduction of the torque-prediction error) against the reference's loop over the

@@ -3,7 +3,7 @@
 cvxpy and MOSEK are absent here, so phi parity (the SDP's output) stays "needs cvxpy + MOSEK".  What is checked:
   * every constraint matrix against the reference's formulas, restated here element by element, at the prior and
     at random phi (1e-12), and the float32 Q_full the reference builds (src/solver.py:69);
-  * the entropic term (src/solver.py:164-172) and the unknown-reg_type error;
+  * the entropic term (src/solver.py:164-172), the float32 prior's metric, and an unknown reg_type (no regulariser);
   * the whole cvxpy path (every reg_type, stacked and Gram-form data terms) driven through tests/fake_cvxpy.py,
     a numeric stand-in that records each constraint at the initial point (the prior) instead of solving.
 """
@@ -100,12 +100,68 @@ def test_entropic_and_pullback_terms():
         assert np.allclose(M, M.T) and np.min(np.linalg.eigvalsh(M)) > 0
 
 
-def test_unknown_reg_type_raises():
-    n = 20
-    Y = np.eye(n)
-    s = S.Solver(Y, np.ones(n), 2, np.zeros(n), 1.0, [None, None])
-    with pytest.raises(ValueError, match="reg_type"):
-        s.solve_fully_consistent(reg_type="bregman")
+def test_unknown_reg_type_solves_unregularised(monkeypatch):
+    """src/solver.py:161-180 is an if / elif chain: any other reg_type adds no regulariser and the problem is solved
+    with the data term alone.  The mirror does the same (and warns)."""
+    import tests.fake_cvxpy as fcp
+    monkeypatch.setitem(sys.modules, "cvxpy", fcp)
+    L = links()
+    prior = np.concatenate([p for p, _, _ in L])
+    ells = [{"semi_axes": s_, "center": c_} for _, s_, c_ in L]
+    rng = np.random.default_rng(5)
+    Y, tau = rng.normal(size=(40, 10 * len(L))), rng.normal(size=40)
+    s = S.Solver(Y, tau, len(L), prior, float(sum(p[0] for p, _, _ in L)), ells)
+    with pytest.warns(RuntimeWarning, match="reg_type"):
+        s.solve_fully_consistent(lambda_reg=0.1, reg_type="bregman")
+    data = 0.5 * float(np.sum((Y @ prior - tau) ** 2)) / 40
+    assert abs(s._objective.value - data) <= 1e-12 * max(1.0, data)
+
+
+def ref_pullback_metric(phi):  # src/solver.py:95-121 (cvxpy's .value: the float64 image of the entries)
+    M = np.zeros((10, 10))
+    P = ref_pseudo_inertia(phi).astype(np.float64)
+    P_inv = np.linalg.inv(P)
+    for i in range(10):
+        for j in range(10):
+            v_i = np.zeros(10)
+            v_j = np.zeros(10)
+            v_i[i] = 1
+            v_j[j] = 1
+            V_i = ref_pseudo_inertia(v_i).astype(np.float64)
+            V_j = ref_pseudo_inertia(v_j).astype(np.float64)
+            M[i, j] = np.trace(P_inv @ V_i @ P_inv @ V_j)
+    M = (M + M.T) / 2
+    eigenvalues = np.linalg.eigvals(M)
+    if np.any(eigenvalues < 0):
+        shift = - np.min(eigenvalues) + 1e-5
+        M = M + shift * np.eye(M.shape[0])
+    return M
+
+
+def ref_entropic_constants(phi):  # src/solver.py:164-172: X = VT.T @ Sigma_inv @ U.T @ J, log(det(J_prior) + 1e-5)
+    J_prior = ref_pseudo_inertia(phi).astype(np.float64)
+    U, Sigma, VT = np.linalg.svd(J_prior, full_matrices=True)
+    Sigma_inv = np.linalg.pinv(np.diag(Sigma))
+    return VT.T @ Sigma_inv @ U.T, np.log(np.linalg.det(J_prior) + 1e-5)
+
+
+def test_float32_prior_metric_and_entropic_constants_bitwise():
+    """The prior is float32 (src/sys_identification.py:61) and the reference unpacks the float32 slice, so its
+    pseudo-inertia trace and diagonal are float32 sums (src/solver.py:55-57): the pull-back metric and the entropic
+    constants built from it must match the reference's restatement bitwise, and differ from a float64 build."""
+    differs = False
+    for phi, _, _ in links():
+        p32 = phi.astype(np.float32)
+        assert np.array_equal(S.pullback_metric(p32), ref_pullback_metric(p32))
+        X_map, ldp = S.entropic_prior_terms(p32)
+        rX, rl = ref_entropic_constants(p32)
+        assert np.array_equal(X_map, rX) and ldp == rl
+        differs |= not np.array_equal(S.pullback_metric(p32), S.pullback_metric(p32.astype(np.float64)))
+    assert differs  # the float32 sums are visible (the test would not see a float64 build otherwise)
+    # the solver mirror hands the raw float32 slice of the prior to both (not a float64 copy)
+    import inspect
+    src = inspect.getsource(S._solve_fully_consistent_cvxpy)
+    assert "pullback_metric(prior_raw)" in src and "entropic_prior_terms(prior_raw)" in src
 
 
 @pytest.mark.parametrize("reg_type", ["constant_pullback", "entropic", "euclidean"])
