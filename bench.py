@@ -142,9 +142,12 @@ def cpu_model():
 
 def e2e_legs(eng, data, N, reps=3):
     """§8(d) end-to-end samples/s of the host entry point (numpy in -> numpy out, PCIe both ways):
-    full outputs (stacked Y_proj, tau_proj, B_v, B_c + Gram) and Gram only (inputs in, 190 KB out)."""
+    full outputs (stacked Y_proj, tau_proj, B_v, B_c + Gram) and Gram only (inputs in, 190 KB out).  The inputs in
+    read_data's dtypes (demo/spot_identification.py:10-25): q and contact float32 as loaded, dq / ddq / tau float64
+    (filtered); the engine sends them in its wire format (sysid_build_f32qc)."""
+    import numpy as np
     from system_identification_amd.engine import EMIT_ALL, EMIT_GRAM
-    ins = [data[k] for k in ("q", "dq", "ddq", "tau", "contact")]
+    ins = [data["q"].astype(np.float32), data["dq"], data["ddq"], data["tau"], data["contact"].astype(np.float32)]
     in_bytes = sum(a.nbytes for a in ins)
     res = {}
     for name, flags in (("full", EMIT_ALL), ("gram_only", EMIT_GRAM)):

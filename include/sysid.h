@@ -91,7 +91,7 @@ extern "C" {
 typedef struct sysid_engine sysid_engine;
 
 /* ABI version (bumped on any signature or layout change). */
-int32_t sysid_abi_version(void);  /* 6 */
+int32_t sysid_abi_version(void);  /* 7 */
 
 /* Create an engine for one device from a packed model.  Replaces the model construction of
  * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
@@ -116,6 +116,16 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
                     const double* tau, const double* cnt, int64_t N, int64_t ld, uint32_t flags,
                     double* Y_proj, double* tau_proj, double* B_v, double* B_c,
                     double* gram, double* Atb, double* btb);
+
+/* sysid_build with q and cnt in float32, the dtypes read_data returns them in (demo/spot_identification.py:10-14:
+ * np.loadtxt(..., dtype=np.float32); the Butterworth filter at :20-25 makes dq, ddq and tau float64).  Same outputs
+ * and behaviour; the inputs cross PCIe as q float32 and one byte per contact value (the non-zero test is all the
+ * projector reads: `if contact_scedule[index]`, src/sys_identification.py:125), 461 instead of 568 bytes per Spot
+ * sample, and are widened exactly on the device.  Replaces the same reference interface as sysid_build. */
+int32_t sysid_build_f32qc(sysid_engine* e, const float* q, const double* dq, const double* ddq,
+                          const double* tau, const float* cnt, int64_t N, int64_t ld, uint32_t flags,
+                          double* Y_proj, double* tau_proj, double* B_v, double* B_c,
+                          double* gram, double* Atb, double* btb);
 
 /* get_full_regressor_force (src/sys_identification.py:391-399), batched: the unprojected joint-torque
  * regressor Y (N·nv x 10·nb) and F = Sᵀ tau + J_cᵀ lambda (N·nv), lambda = the measured forces

@@ -45,8 +45,11 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // nothing behind, and launches on different streams with different workspaces may run concurrently.
 constexpr size_t WORK_BYTES = 128 * K1_SHARDS;  // one 128-byte line per claim counter
 
-// A persistent pool of host threads for the host entry points' input packing (stage_inputs): started on first use,
-// joined by sysid_destroy.  run(f) calls f(t) on every worker t and returns when all have finished.
+// A persistent pool of host threads for the host entry points' input packing (Stager): started on first use, joined
+// by sysid_destroy.  start(f) calls f(t) on every worker t; wait() returns when all have finished.  A worker that
+// has finished a job spins for SPIN_US before it blocks on the condition variable: a call that follows within that
+// window (back-to-back host calls) starts packing at once instead of paying a thread wake-up (~20-40 us, on the
+// critical path of the first chunk's DMA).
 class HostPool {
  public:
   explicit HostPool(int n) : n_(n) {
@@ -67,7 +70,7 @@ class HostPool {
       std::lock_guard<std::mutex> g(m_);
       job_ = std::move(f);
       pending_ = n_;
-      ++gen_;
+      gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
   }
@@ -77,15 +80,20 @@ class HostPool {
   }
 
  private:
+  static constexpr int SPIN_US = 2000;
   void loop(int t) {
     uint64_t seen = 0;
     for (;;) {
       std::function<void(int)> f;
+      const auto spin_end = std::chrono::steady_clock::now() + std::chrono::microseconds(SPIN_US);
+      while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed) &&
+             std::chrono::steady_clock::now() < spin_end) {
+      }
       {
         std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
         if (stop_) return;
-        seen = gen_;
+        seen = gen_.load();
         f = job_;
       }
       f(t);
@@ -101,8 +109,8 @@ class HostPool {
   std::condition_variable cv_, done_cv_;
   std::function<void(int)> job_;
   int pending_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
 };
 
 }  // namespace
@@ -151,10 +159,16 @@ struct sysid_engine {
   size_t out_cap = 0;
   int host_register = -1;    // host API copies: 1 page-lock the caller's arrays, 0 pageable, -1 by size
   double* d_dump = nullptr;  // diagnostics only
-  double* h_stage = nullptr;  // host API: page-locked staging of the input block (grow-only)
+  double* h_stage = nullptr;  // host API: page-locked staging of the inputs' wire blocks (grow-only)
   size_t h_stage_cap = 0;
+  unsigned char* d_wire = nullptr;  // host API: the wire blocks on the device (K0W widens them into d_in)
+  size_t wire_cap = 0;
+  double* h_gram = nullptr;   // host API: page-locked copy of the (W+1)^2 Gram, one DMA back (grow-only)
   HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
   hipStream_t copy_stream = nullptr;     // host API: the staged input chunks' DMA (created on first use)
+  static constexpr int MAX_COPY = 4;
+  hipStream_t copy_more[MAX_COPY] = {};  // further copy streams (SYSID_COPY_STREAMS > 1): chunk c on stream c % n
+  int ncopy = 1;
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -268,9 +282,10 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
 // cmp: the Gram-only nullspace mode (rcount: its per-sample row counts).
 int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
               unsigned long long* work, hipStream_t st, double* dbg, int full = 0, int prec = 0, int cmp = 0,
-              int* rcount = nullptr) {
+              int* rcount = nullptr, bool zeroed = false) {
   K1Params kp = e->kp;
-  HIP_TRY(e, zero_async(work, WORK_BYTES, st));
+  // the claim counters start at 0 (zeroed = true: the host path's K0W of this chunk has just zeroed them)
+  if (!zeroed) HIP_TRY(e, zero_async(work, WORK_BYTES, st));
   if (full) {
     kp.full = 1;
     kp.in_rows = e->in_lds;
@@ -392,7 +407,7 @@ int check_stages(sysid_engine* e, int64_t N, int64_t ld_panel, uint32_t flags, c
 
 int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                   int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, hipStream_t st,
-                  hipEvent_t* ev /* 4 events or null */) {
+                  hipEvent_t* ev /* 4 events or null */, bool zeroed = false) {
   if (N <= 0) return SYSID_OK;
   int rc = check_stages(e, N, ld_panel, flags, d_ws, ws_bytes);
   if (rc != SYSID_OK) return rc;
@@ -413,7 +428,8 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
     return SYSID_OK;
   }
   if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
-  if ((rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, work, st, nullptr)) != SYSID_OK) return rc;
+  if ((rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, work, st, nullptr, 0, 0, 0, nullptr, zeroed)) != SYSID_OK)
+    return rc;
   if (ev) HIP_TRY(e, hipEventRecord(ev[1], st));
   if (flags & SYSID_EMIT_GRAM) {
     const int ks = ksplit_for(e, rows);
@@ -509,17 +525,16 @@ bool gram_fused(const sysid_engine* e, uint32_t flags) {
 }
 
 // staged (host entry point): the staged chunks' bounds (staged chunk k = samples [b[k], b[k+1])), and
-// (*stage_upto)(n) before the K1 of a chunk ending at sample n (it orders `st` after the DMA of the inputs [0, n));
+// (*stage_upto)(n) before the K1 of a chunk ending at sample n (it orders `st` after the DMA and the K0W widening of
+// the inputs [0, n), returning > 0 when it staged a chunk, whose K0W has then zeroed K1's claim counters);
 // nullptr: the workspace's chunk size, inputs already on the device.
 int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_gram,
                         void* d_ws, size_t ws_bytes, hipStream_t st, std::vector<hipEvent_t>* ev = nullptr,
                         const std::vector<int64_t>* staged = nullptr,
-                        const std::function<int(int64_t)>* stage_upto = nullptr, bool chunk_major = false) {
+                        const std::function<int(int64_t)>* stage_upto = nullptr) {
   if (N <= 0) return SYSID_OK;
   const int prec = gram_prec(flags);
   const int cmp = gram_nullspace(e, flags);
-  if (chunk_major && (!staged || gram_fused(e, flags)))
-    return set_err(e, SYSID_E_INVALID, "chunk-major inputs need the staged, unfused chunk loop");
   if (d_ws == nullptr || ws_bytes < gram_ws_bytes_prec(e, N, prec))
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
                    gram_ws_bytes_prec(e, N, prec));
@@ -535,7 +550,7 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
       return SYSID_OK;
     };
     int rc;
-    if (stage_upto && (rc = (*stage_upto)(N))) return rc;  // every chunk's DMA
+    if (stage_upto && (rc = (*stage_upto)(N)) < 0) return rc;  // every chunk's DMA
     if ((rc = mark())) return rc;
     if ((rc = launch_k12(e, d_in, N, ld, ring, e->ldp, slab, st, 1))) return rc;
     while (ev && k + 1 < ev->size())
@@ -563,28 +578,28 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
   size_t sc = 0;  // the staged chunk holding c0
   for (int64_t c0 = 0, n = 0; c0 < N; c0 += n) {
     n = std::min(C, N - c0);
-    // staged chunk [k0, k1) (chunk-major: its own (rows x (k1 - k0)) block at offset rows·k0): a launch never
-    // straddles two of them, so each chunk's kernels wait only for its own DMA (a staged chunk larger than the
-    // workspace chunk runs as several launches)
-    int64_t k0 = 0, k1 = N;
+    // staged chunk [k0, k1): a launch never straddles two of them, so each chunk's kernels wait only for its own
+    // DMA (a staged chunk larger than the workspace chunk runs as several launches)
     if (staged) {
       while (sc + 2 < staged->size() && (*staged)[sc + 1] <= c0) ++sc;
-      k0 = (*staged)[sc];
-      k1 = (*staged)[sc + 1];
-      n = std::min(n, k1 - c0);
+      n = std::min(n, (*staged)[sc + 1] - c0);
     }
-    if (stage_upto && (rc = (*stage_upto)(c0 + n))) return rc;  // this chunk's inputs
+    bool zeroed = false;  // a chunk staged just now: its K0W zeroed the claim counters
+    if (stage_upto) {
+      if ((rc = (*stage_upto)(c0 + n)) < 0) return rc;  // this chunk's inputs
+      zeroed = rc > 0;
+    }
     if ((rc = mark())) return rc;
-    const double* cin = chunk_major ? d_in + (int64_t)e->in_rows * k0 + (c0 - k0) : d_in + c0;
-    const int64_t cld = chunk_major ? k1 - k0 : ld;
+    const double* cin = d_in + c0;
+    const int64_t cld = ld;
     if (cmp) {
-      if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount)))
+      if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, zeroed)))
         return rc;
       const unsigned nseg = (unsigned)((n + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG);
       hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
       hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, rseg, (int)n, e->nv, rowlist, d_rows);
       HIP_TRY(e, hipGetLastError());
-    } else if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr))) {
+    } else if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr, zeroed))) {
       return rc;
     }
     if ((rc = mark())) return rc;
@@ -648,37 +663,92 @@ int host_copy(sysid_engine* e, void* dst, const void* src, size_t bytes, hipMemc
 // The host entry points' copy stream, created on first use and warmed by one small DMA: the runtime sets up the
 // stream's copy queue lazily on its first copy, which under a resident full-chip K1 took milliseconds
 // (profiles/r04_s3).
-int ensure_copy_stream(sysid_engine* e) {
-  if (e->copy_stream) return SYSID_OK;
-  HIP_TRY(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+int warm_copy_stream(sysid_engine* e, hipStream_t* sp) {
+  HIP_TRY(e, hipStreamCreateWithFlags(sp, hipStreamNonBlocking));
   double* h = nullptr;
   HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&h), 256, hipHostMallocDefault));
   double* d = nullptr;
   hipError_t r = hipMalloc(reinterpret_cast<void**>(&d), 256);
-  if (r == hipSuccess) r = hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, e->copy_stream);
-  if (r == hipSuccess) r = hipStreamSynchronize(e->copy_stream);
+  if (r == hipSuccess) r = hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, *sp);
+  if (r == hipSuccess) r = hipStreamSynchronize(*sp);
   if (d) (void)hipFree(d);
   (void)hipHostFree(h);
   if (r != hipSuccess) return set_err(e, SYSID_E_DEVICE, "copy stream set-up failed: %s", hipGetErrorString(r));
   return SYSID_OK;
 }
+int ensure_copy_stream(sysid_engine* e) {
+  if (e->copy_stream) return SYSID_OK;
+  if (int rc = warm_copy_stream(e, &e->copy_stream)) return rc;
+  // SYSID_COPY_STREAMS=n (dev knob): the staged chunks' DMAs round-robin over n copy streams
+  if (const char* v = std::getenv("SYSID_COPY_STREAMS")) e->ncopy = std::max(1, std::min(e->MAX_COPY, std::atoi(v)));
+  for (int k = 1; k < e->ncopy; ++k)
+    if (int rc = warm_copy_stream(e, &e->copy_more[k])) return rc;
+  return SYSID_OK;
+}
+hipStream_t copy_stream_of(const sysid_engine* e, int c) {
+  const int k = c % e->ncopy;
+  return k == 0 ? e->copy_stream : e->copy_more[k];
+}
+
+// Wire format of the host entry points' inputs (K0W, sysid_kernels.h): per staged chunk of n samples, the q rows in
+// the caller's element type (float32 from read_data, demo/spot_identification.py:10, or float64), the dq / ddq / tau
+// rows in float64 and the contact rows as one byte each (non-zero flag); sections 16-byte aligned.  Spot with float32
+// q: 461 instead of 568 bytes per sample over PCIe.
+struct Wire {
+  int64_t d, c, bytes;  // byte offsets of the float64 rows and of the contact bytes; block size
+};
+Wire wire_layout(int nq, int nd, int nc, int64_t n, int qsz) {
+  auto a16 = [](int64_t x) { return (x + 15) & ~(int64_t)15; };
+  Wire w;
+  w.d = a16((int64_t)nq * n * qsz);
+  w.c = w.d + a16((int64_t)nd * n * 8);
+  w.bytes = w.c + a16((int64_t)nc * n);
+  return w;
+}
+
+// The caller's channel rows: q (element size qsz), dq, ddq, tau (float64), contact (element size csz), channel-major
+// with leading dimension ld.
+struct HostInputs {
+  const void* q;
+  int qsz;
+  const double* dq;
+  const double* ddq;
+  const double* tau;
+  const void* cnt;
+  int csz;
+  int64_t ld;
+};
 
 class Stager {
  public:
-  Stager(sysid_engine* e, int64_t N, double* d_dst) : e_(e), N_(N), d_dst_(d_dst) {}
+  Stager(sysid_engine* e, int64_t N) : e_(e), N_(N) {}
   ~Stager() { finish(); }
   const std::vector<int64_t>& bounds() const { return b_; }  // staged chunk c = samples [b_[c], b_[c + 1])
-  bool chunk_major() const { return cm_; }
   int chunks() const { return nch_; }
-  // chunk_major (the Gram-only path, one K1 launch per chunk): chunk c is packed as its own (rows x n) block at
-  // offset rows·c0 of the staging block and of the device block, so it leaves as ONE contiguous DMA, and chunk c's
-  // K1 reads it with ld = n (chunk_input()).  Otherwise the block keeps the caller's row-major layout (ld = N) and
-  // each chunk is a 2-D DMA of one row piece per channel.
-  int begin(const double* const* srcs, const int* nrows, int nsrc, int64_t ld, bool chunk_major = false,
-            const std::vector<int64_t>* bounds = nullptr) {
+  // Host threads (the engine's pool) pack chunk after chunk of the caller's rows into the engine's page-locked
+  // staging block in the wire format; stage(c) waits until chunk c is packed, sends it as ONE DMA on the engine's
+  // copy stream into the device wire buffer, makes `st` wait for that DMA and widens the chunk into the row-major
+  // float64 input block e->d_in (ld = N) with K0W, which also zeroes K1's claim counters (`work`).
+  int begin(const HostInputs& in, const std::vector<int64_t>* bounds = nullptr) {
     sysid_engine* e = e_;
-    cm_ = chunk_major;
-    const size_t need = (size_t)e->in_rows * N_ * sizeof(double);
+    in_ = in;
+    int parts = 2;  // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few
+                    // (Spot 20k Gram-only e2e, 1 / 2 / 4 / 8 chunks: 0.74 / 0.67 / 0.75 / 1.05 ms; profiles/r04_h)
+    if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
+    const int64_t CH = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
+    b_.clear();
+    if (bounds && !std::getenv("SYSID_STAGE_CHUNKS")) {
+      b_ = *bounds;
+    } else {
+      for (int64_t c0 = 0; c0 < N_; c0 += CH) b_.push_back(c0);
+      b_.push_back(N_);
+    }
+    nch_ = (int)b_.size() - 1;
+    nd_ = 2 * e->nv + e->nj;
+    off_.assign(nch_ + 1, 0);
+    for (int c = 0; c < nch_; ++c)
+      off_[c + 1] = off_[c] + wire_layout(e->nq, nd_, e->nc, b_[c + 1] - b_[c], in_.qsz).bytes;
+    const size_t need = (size_t)off_[nch_];
     if (need > e->h_stage_cap) {
       if (e->h_stage) (void)hipHostFree(e->h_stage);
       e->h_stage = nullptr;
@@ -686,26 +756,14 @@ class Stager {
       HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), need, hipHostMallocDefault));
       e->h_stage_cap = need;
     }
-    for (int k = 0; k < nsrc; ++k)
-      for (int r = 0; r < nrows[k]; ++r) row_src_.push_back(srcs[k] + (int64_t)r * ld);
-    if (!e->pool) {
+    if (int rc = grow(e, reinterpret_cast<void**>(&e->d_wire), &e->wire_cap, need)) return rc;
+    // below 1 MiB the calling thread packs everything at once (no pool hand-off)
+    inline_ = need < ((size_t)1 << 20);
+    if (!inline_ && !e->pool) {
       int T = 8;  // the GPU box grants a job 16 host threads (OMP_NUM_THREADS): half of them pack
       if (const char* v = std::getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(8, std::atoi(v) / 2));
       e->pool = new HostPool(T);
     }
-    int parts = 2;  // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few
-                    // (Spot 20k Gram-only e2e, 1 / 2 / 4 / 8 chunks: 0.74 / 0.67 / 0.75 / 1.05 ms; profiles/r04_h)
-    if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
-    CH_ = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
-    nch_ = (int)((N_ + CH_ - 1) / CH_);
-    b_.clear();
-    if (bounds && !std::getenv("SYSID_STAGE_CHUNKS")) {
-      b_ = *bounds;
-    } else {
-      for (int c = 0; c < nch_; ++c) b_.push_back((int64_t)c * CH_);
-      b_.push_back(N_);
-    }
-    nch_ = (int)b_.size() - 1;
     if (int rc = ensure_copy_stream(e)) return rc;
     while ((int)e->stage_ev.size() < nch_) {
       hipEvent_t x;
@@ -714,38 +772,69 @@ class Stager {
     }
     done_.reset(new std::atomic<int>[nch_]);
     for (int c = 0; c < nch_; ++c) done_[c].store(0);
-    const int T = e->pool->size(), R = (int)row_src_.size();
-    double* hs = e->h_stage;
-    e->pool->start([this, T, R, hs](int t) {
+    const int T = inline_ ? 1 : e->pool->size(), R = e->nq + nd_ + e->nc;
+    packers_ = T;
+    unsigned char* hs = reinterpret_cast<unsigned char*>(e->h_stage);
+    auto pack = [this, T, R, hs](int t) {
+      const int nq = e_->nq, nc = e_->nc;
+      const int nv = e_->nv;
       for (int c = 0; c < nch_; ++c) {
         const int64_t c0 = b_[c], n = b_[c + 1] - c0;
-        for (int r = t; r < R; r += T)
-          std::memcpy(cm_ ? hs + (int64_t)R * c0 + (int64_t)r * n : hs + (int64_t)r * N_ + c0, row_src_[r] + c0,
-                      (size_t)n * sizeof(double));
+        const Wire w = wire_layout(nq, nd_, nc, n, in_.qsz);
+        unsigned char* blk = hs + off_[c];
+        for (int r = t; r < R; r += T) {
+          if (r < nq) {
+            const char* src = static_cast<const char*>(in_.q) + ((int64_t)r * in_.ld + c0) * in_.qsz;
+            std::memcpy(blk + (int64_t)r * n * in_.qsz, src, (size_t)n * in_.qsz);
+          } else if (r < nq + nd_) {
+            const int k = r - nq;  // dq rows, ddq rows, tau rows
+            const double* src = k < nv ? in_.dq + (int64_t)k * in_.ld
+                                : k < 2 * nv ? in_.ddq + (int64_t)(k - nv) * in_.ld
+                                             : in_.tau + (int64_t)(k - 2 * nv) * in_.ld;
+            std::memcpy(blk + w.d + (int64_t)k * n * 8, src + c0, (size_t)n * 8);
+          } else {
+            const int k = r - nq - nd_;
+            if (k == 0) check(c0, n);  // the packer of a chunk's first contact row checks the chunk's contacts
+            unsigned char* dst = blk + w.c + (int64_t)k * n;
+            if (in_.csz == 4) {
+              const float* src = static_cast<const float*>(in_.cnt) + (int64_t)k * in_.ld + c0;
+              for (int64_t x = 0; x < n; ++x) dst[x] = src[x] != 0.0f;  // NaN counts as non-zero, as in K1
+            } else {
+              const double* src = static_cast<const double*>(in_.cnt) + (int64_t)k * in_.ld + c0;
+              for (int64_t x = 0; x < n; ++x) dst[x] = src[x] != 0.0;
+            }
+          }
+        }
         done_[c].fetch_add(1, std::memory_order_release);
       }
-    });
-    started_ = true;
+    };
+    if (inline_) {
+      pack(0);
+    } else {
+      e->pool->start(pack);
+      started_ = true;
+    }
     return SYSID_OK;
   }
-  // chunk c: wait until packed, DMA it, and order `st` after that DMA
-  int stage(int c, hipStream_t st) {
+  // chunk c: wait until packed, DMA it, order `st` after that DMA and widen it into e->d_in (zeroing `work`)
+  int stage(int c, hipStream_t st, unsigned long long* work) {
     sysid_engine* e = e_;
-    const int T = e->pool->size();
-    while (done_[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    while (done_[c].load(std::memory_order_acquire) < packers_) std::this_thread::yield();
+    if (bad_.load(std::memory_order_acquire) >= 0) return SYSID_E_CONTACT;  // the caller reports it (contact_error)
     stamp();  // SYSID_TRACE_HOST: chunk c packed
     const int64_t c0 = b_[c], n = b_[c + 1] - c0;
-    const double* hs = e->h_stage;
-    const int64_t R = (int64_t)row_src_.size();
-    const hipError_t cr =
-        cm_ ? hipMemcpyAsync(d_dst_ + R * c0, hs + R * c0, (size_t)(R * n) * sizeof(double), hipMemcpyHostToDevice,
-                             e->copy_stream)
-            : hipMemcpy2DAsync(d_dst_ + c0, (size_t)N_ * sizeof(double), hs + c0, (size_t)N_ * sizeof(double),
-                               (size_t)n * sizeof(double), (size_t)R, hipMemcpyHostToDevice, e->copy_stream);
-    if (cr != hipSuccess || hipEventRecord(e->stage_ev[c], e->copy_stream) != hipSuccess ||
+    const Wire w = wire_layout(e->nq, nd_, e->nc, n, in_.qsz);
+    const unsigned char* hs = reinterpret_cast<const unsigned char*>(e->h_stage) + off_[c];
+    hipStream_t cs = copy_stream_of(e, c);
+    if (hipMemcpyAsync(e->d_wire + off_[c], hs, (size_t)w.bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipEventRecord(e->stage_ev[c], cs) != hipSuccess ||
         hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
       return set_err(e, SYSID_E_DEVICE, "input copy failed");
-    stamp();  // chunk c's DMA enqueued
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (n + 1023) / 1024));
+    hipLaunchKernelGGL(k0_widen, dim3(gx, (unsigned)(e->nq + nd_ + e->nc)), dim3(256), 0, st, e->d_wire + off_[c], n,
+                       e->nq, nd_, in_.qsz, w.d, w.c, e->d_in + c0, N_, work, (int)(WORK_BYTES / 8));
+    HIP_TRY(e, hipGetLastError());
+    stamp();  // chunk c's DMA and widening enqueued
     return SYSID_OK;
   }
   // host-clock stamps (ms since t0) of the trace, two per chunk: packed, DMA enqueued
@@ -754,6 +843,7 @@ class Stager {
     trace_ = true;
   }
   const std::vector<double>& stamps() const { return stamps_; }
+  bool contacts_bad() const { return bad_.load(std::memory_order_acquire) >= 0; }
   void finish() {
     if (started_) e_->pool->wait();
     started_ = false;
@@ -761,14 +851,36 @@ class Stager {
 
  private:
   sysid_engine* e_;
-  int64_t N_, CH_ = 0;
-  int nch_ = 0;
-  std::vector<int64_t> b_;  // staged chunk bounds (begin())
-  double* d_dst_;
-  std::vector<const double*> row_src_;  // channel row r of the block <- its source row
+  int64_t N_;
+  int nch_ = 0, nd_ = 0, packers_ = 1;
+  bool inline_ = false;
+  std::atomic<int64_t> bad_{-1};  // a sample that breaks the contact contract (check), -1: none found
+  // The reference's contact contract (m = int(np.sum(cnt)) blocks of three rows, one per truthy foot,
+  // src/sys_identification.py:121-128) on samples [c0, c0 + n): checked while the chunk is packed, off the call's
+  // critical path; stage() refuses the chunk's DMA once a violation is found.
+  void check(int64_t c0, int64_t n) {
+    const int nc = e_->nc;
+    for (int64_t s = c0; s < c0 + n; ++s) {
+      double sum = 0.0;
+      int nz = 0;
+      for (int k = 0; k < nc; ++k) {
+        const double v = in_.csz == 4 ? (double)static_cast<const float*>(in_.cnt)[(int64_t)k * in_.ld + s]
+                                      : static_cast<const double*>(in_.cnt)[(int64_t)k * in_.ld + s];
+        sum += v;
+        nz += v != 0.0;
+      }
+      if (!(std::trunc(sum) >= (double)nz)) {
+        int64_t cur = bad_.load();
+        while ((cur < 0 || s < cur) && !bad_.compare_exchange_weak(cur, s)) {}
+        return;
+      }
+    }
+  }
+  HostInputs in_{};
+  std::vector<int64_t> b_;    // staged chunk bounds (begin())
+  std::vector<int64_t> off_;  // byte offset of chunk c's wire block (staging and device)
   std::unique_ptr<std::atomic<int>[]> done_;
   bool started_ = false;
-  bool cm_ = false;
   bool trace_ = false;
   std::chrono::steady_clock::time_point t0_;
   std::vector<double> stamps_;
@@ -798,7 +910,7 @@ int launch_k5(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_p
 
 extern "C" {
 
-int32_t sysid_abi_version(void) { return 6; }
+int32_t sysid_abi_version(void) { return 7; }
 
 const char* sysid_last_error(const sysid_engine* e) { return e ? e->err.c_str() : g_thread_error.c_str(); }
 
@@ -1187,9 +1299,13 @@ void sysid_destroy(sysid_engine* e) {
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
+  if (e->h_gram) (void)hipHostFree(e->h_gram);
+  if (e->d_wire) (void)hipFree(e->d_wire);
   delete e->pool;
   for (hipEvent_t x : e->stage_ev) (void)hipEventDestroy(x);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
+  for (hipStream_t x : e->copy_more)
+    if (x) (void)hipStreamDestroy(x);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1212,29 +1328,7 @@ size_t sysid_workspace_bytes(const sysid_engine* e, int64_t N, uint32_t flags) {
   return stages_ws_bytes(e, N, flags);
 }
 
-int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld, int64_t* bad) {
-  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
-  if (e->nc == 0 || N <= 0) return SYSID_OK;
-  if (!cnt || ld < N) return set_err(const_cast<sysid_engine*>(e), SYSID_E_INVALID, "bad contact buffer");
-  for (int64_t s = 0; s < N; ++s) {
-    double sum = 0.0;
-    int64_t nz = 0;
-    for (int c = 0; c < e->nc; ++c) {
-      const double v = cnt[(int64_t)c * ld + s];
-      sum += v;
-      nz += v != 0.0;
-    }
-    // reference: m = int(np.sum(cnt)) blocks of three rows are allocated, one per truthy foot
-    const double tr = std::trunc(sum);
-    if (!(tr >= (double)nz)) {
-      if (bad) *bad = s;
-      return set_err(const_cast<sysid_engine*>(e), SYSID_E_CONTACT,
-                     "sample %lld: int(sum(contact)) = %g is smaller than the %lld feet in contact", (long long)s, tr,
-                     (long long)nz);
-    }
-  }
-  return SYSID_OK;
-}
+int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld, int64_t* bad);
 
 int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags,
                            double* d_panel, int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes,
@@ -1445,12 +1539,39 @@ int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_
   return rc;
 }
 
-int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
-                    const double* cnt, int64_t N, int64_t ld, uint32_t flags, double* Y_proj, double* tau_proj,
-                    double* B_v, double* B_c, double* gram, double* Atb, double* btb) {
+}  // extern "C"
+
+namespace {
+
+// The reference's contact contract (m = int(np.sum(cnt)) blocks of three rows, one per truthy foot) on the
+// caller's contact rows (float32 from read_data, or float64).
+template <typename T>
+int check_contacts_t(sysid_engine* e, const T* cnt, int64_t N, int64_t ld, int64_t* bad) {
+  for (int64_t s = 0; s < N; ++s) {
+    double sum = 0.0;
+    int64_t nz = 0;
+    for (int c = 0; c < e->nc; ++c) {
+      const T v = cnt[(int64_t)c * ld + s];
+      sum += (double)v;
+      nz += v != (T)0;
+    }
+    const double tr = std::trunc(sum);
+    if (!(tr >= (double)nz)) {
+      if (bad) *bad = s;
+      return set_err(e, SYSID_E_CONTACT, "sample %lld: int(sum(contact)) = %g is smaller than the %lld feet in contact",
+                     (long long)s, tr, (long long)nz);
+    }
+  }
+  return SYSID_OK;
+}
+
+// The host entry points (sysid_build, sysid_build_f32qc): the caller's rows go to the device in the wire format
+// (Stager, K0W), the kernels run on the engine's stream, the outputs come back in one copy each.
+int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags, double* Y_proj, double* tau_proj,
+               double* B_v, double* B_c, double* gram, double* Atb, double* btb) {
   if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
-  if (N < 0 || ld < N) return set_err(e, SYSID_E_INVALID, "bad N/ld (%lld/%lld)", (long long)N, (long long)ld);
-  if (N > 0 && (!q || !dq || !ddq || (!tau && e->nj) || (!cnt && e->nc)))
+  if (N < 0 || in.ld < N) return set_err(e, SYSID_E_INVALID, "bad N/ld (%lld/%lld)", (long long)N, (long long)in.ld);
+  if (N > 0 && (!in.q || !in.dq || !in.ddq || (!in.tau && e->nj) || (!in.cnt && e->nc)))
     return set_err(e, SYSID_E_INVALID, "null input buffer");
   // SYSID_TRACE_HOST=1: host-clock phase times of this call on stderr (diagnostics of the e2e number)
   static const bool trace = std::getenv("SYSID_TRACE_HOST") != nullptr;
@@ -1458,10 +1579,13 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const clk::time_point t0 = clk::now();
   double tph[4] = {0, 0, 0, 0};
   auto ms_since = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-  if (N > 0 && e->nc) {
-    const int rc = sysid_check_contacts(e, cnt, N, ld, nullptr);
-    if (rc != SYSID_OK) return rc;
-  }
+  // the contact contract is checked by the packing threads (Stager::check), chunk by chunk; a violation makes the
+  // call return SYSID_E_CONTACT (message: the first offending sample) before any output is written
+  auto contact_error = [&]() -> int {
+    const int r = in.csz == 4 ? check_contacts_t(e, static_cast<const float*>(in.cnt), N, in.ld, nullptr)
+                              : check_contacts_t(e, static_cast<const double*>(in.cnt), N, in.ld, nullptr);
+    return r != SYSID_OK ? r : set_err(e, SYSID_E_CONTACT, "contact contract violated");
+  };
   const bool want_gram = (flags & SYSID_EMIT_GRAM) && (gram || Atb || btb);
   if (want_gram) flags |= SYSID_EMIT_GRAM; else flags &= ~SYSID_EMIT_GRAM;
   tph[0] = ms_since(t0);  // contact check
@@ -1478,24 +1602,18 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const bool panel_out = ((flags & SYSID_EMIT_Y) && Y_proj) || ((flags & SYSID_EMIT_TAU) && tau_proj) ||
                          ((flags & SYSID_EMIT_FRICTION) && (B_v || B_c) && e->nj);
   const bool gram_only = want_gram && !panel_out;
-  const bool staged = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20) && e->host_register != 0;
   const int gp = gram_prec(flags);
-  // Gram-only, chunk by chunk: each chunk packed as its own block and sent as one contiguous DMA
-  // (SYSID_STAGE_LAYOUT=rows: the row-major block, a 2-D DMA per chunk)
-  static const bool rows_layout = [] {
-    const char* v = std::getenv("SYSID_STAGE_LAYOUT");
-    return v && std::strcmp(v, "rows") == 0;
-  }();
-  const bool chunk_major = staged && gram_only && !gram_fused(e, flags) && !rows_layout;
-  // Gram-only staged chunks on K1's round boundaries: a first chunk of one round of K1 (every resident wave one step:
-  // its DMA is short, so the kernels start early), then the rest in two chunks of whole rounds, so the chunks add no
-  // partial K1 rounds to the unchunked launch's (SYSID_STAGE_CHUNKS=k: k equal chunks instead)
-  // (SYSID_STAGE_SPLIT=2: the one-round chunk, then the rest in one chunk)
+  // Gram-only staged chunks on K1's round boundaries (SYSID_STAGE_CHUNKS=k: k equal chunks instead).
+  // Two staged chunks: a first chunk of one K1 round (every resident wave one step: its DMA is short, so the kernels
+  // start early), then the rest (Spot 20k Gram-only e2e, float32 q: 0.548-0.556 ms best of 12 against 0.561-0.576 for
+  // one round + two halves of whole rounds, 0.625-0.642 for three round-aligned chunks after the first, 0.642 for one
+  // chunk; profiles/r05_s4).  SYSID_STAGE_SPLIT=3: the one-round chunk, then two chunks of whole rounds.
   std::vector<int64_t> round_bounds;
-  if (staged && gram_only) {
+  const bool big = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20);
+  if (gram_only && big) {
     static const int split = [] {
       const char* v = std::getenv("SYSID_STAGE_SPLIT");
-      return v && std::atoi(v) == 2 ? 2 : 3;
+      return v && std::atoi(v) == 3 ? 3 : 2;
     }();
     const int64_t R = k1_round_samples(e, gp, gram_nullspace(e, flags));
     if (R > 0 && N >= 3 * R && split == 3) {
@@ -1506,11 +1624,25 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
     } else {
       round_bounds = {0, (N + 1) / 2, N};
     }
+  } else {
+    round_bounds = {0, N};  // one chunk (stacked outputs read every sample in one K1; small inputs)
+    if (big && !gram_only) round_bounds.clear();  // stacked outputs, large: the Stager's default chunks
+  }
+  if (const char* v = std::getenv("SYSID_STAGE_BOUNDS")) {  // dev knob: explicit inner chunk bounds "b1,b2,..."
+    if (gram_only && big) {
+      round_bounds = {0};
+      for (const char* p = v; *p;) {
+        const long long b = std::strtoll(p, const_cast<char**>(&p), 10);
+        if (b > round_bounds.back() && b < N) round_bounds.push_back(b);
+        while (*p == ',' || *p == ' ') ++p;
+        if (*p && (*p < '0' || *p > '9')) break;
+      }
+      round_bounds.push_back(N);
+    }
   }
   int rc;
-  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) {
+  if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double))))
     return rc;
-  }
   if (!gram_only &&
       (rc = grow(e, reinterpret_cast<void**>(&e->d_panel), &e->panel_cap, (size_t)rows * e->ldp * sizeof(double))))
     return rc;
@@ -1518,51 +1650,41 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   const size_t wsb = gram_only ? gram_ws_bytes(e, N) : sysid_workspace_bytes(e, N, flags);
   if ((rc = grow(e, &e->d_ws, &e->ws_cap, wsb ? wsb : 256))) return rc;
   hipStream_t st = e->stream;
+  auto* work = static_cast<unsigned long long*>(e->d_ws);
   std::vector<void*> reg;
+  Stager stager(e, N);
   auto fail = [&](int code) {
     (void)hipStreamSynchronize(st);
     if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
+    for (hipStream_t x : e->copy_more)
+      if (x) (void)hipStreamSynchronize(x);
     host_unregister(e, reg);
-    return code;
+    stager.finish();
+    return code == SYSID_E_CONTACT && stager.contacts_bad() ? contact_error() : code;
   };
-  // inputs: channel c of the caller's arrays -> row c of the device block: staged through page-locked memory by
-  // host threads for blocks of 1 MiB and more (stage_inputs), else one copy per array
-  const double* srcs[5] = {q, dq, ddq, tau, cnt};
-  const int nrows[5] = {e->nq, e->nv, e->nv, e->nj, e->nc};
-  Stager stager(e, N, e->d_in);
   if (trace) stager.trace_from(t0);
   int nstaged = 0;  // chunks sent so far
+  // > 0: staged at least one chunk (its K0W zeroed K1's claim counters); < 0: error
   const std::function<int(int64_t)> stage_upto = [&](int64_t upto) -> int {
-    for (; nstaged < stager.chunks() && stager.bounds()[nstaged] < upto; ++nstaged) {
-      const int r = stager.stage(nstaged, st);
+    int k = 0;
+    for (; nstaged < stager.chunks() && stager.bounds()[nstaged] < upto; ++nstaged, ++k) {
+      const int r = stager.stage(nstaged, st, work);
       if (r != SYSID_OK) return r;
     }
-    return SYSID_OK;
+    return k;
   };
-  if (staged && (rc = stager.begin(srcs, nrows, 5, ld, chunk_major, gram_only ? &round_bounds : nullptr)) !=
-                            SYSID_OK) {
-    return fail(rc);
-  }
+  if ((rc = stager.begin(in, round_bounds.empty() ? nullptr : &round_bounds)) != SYSID_OK) return fail(rc);
   // the stacked-output path reads every sample in one launch: all chunks first
-  if (staged && !gram_only && (rc = stage_upto(N)) != SYSID_OK) return fail(rc);
-  tph[1] = ms_since(t0);  // + buffers, packing started (stacked outputs: every chunk's DMA enqueued)
-  int64_t r0 = 0;
-  for (int k = 0; k < 5 && !staged; ++k) {
-    if (nrows[k] > 0) {
-      if (ld == N) {
-        if ((rc = host_copy(e, e->d_in + r0 * N, srcs[k], (size_t)nrows[k] * N * sizeof(double),
-                            hipMemcpyHostToDevice, st, &reg)) != SYSID_OK)
-          return fail(rc);
-      } else if (hipMemcpy2DAsync(e->d_in + r0 * N, (size_t)N * sizeof(double), srcs[k], (size_t)ld * sizeof(double),
-                                  (size_t)N * sizeof(double), nrows[k], hipMemcpyHostToDevice, st) != hipSuccess) {
-        return fail(set_err(e, SYSID_E_DEVICE, "input copy failed"));
-      }
-    }
-    r0 += nrows[k];
+  bool zeroed = false;
+  if (!gram_only) {
+    if ((rc = stage_upto(N)) < 0) return fail(rc);
+    zeroed = true;
   }
+  tph[1] = ms_since(t0);  // + buffers, packing started (stacked outputs: every chunk's DMA enqueued)
   rc = gram_only ? launch_gram_chunked(e, e->d_in, N, N, flags, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
-                                       staged ? &stager.bounds() : nullptr, staged ? &stage_upto : nullptr, chunk_major)
-                 : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr);
+                                       &stager.bounds(), &stage_upto)
+                 : launch_stages(e, e->d_in, N, N, flags, e->d_panel, e->ldp, e->d_gram, e->d_ws, e->ws_cap, st, nullptr,
+                                 zeroed);
   if (rc != SYSID_OK) return fail(rc);
   const double t_kern = ms_since(t0);  // + kernels enqueued (before the output copies)
   if (panel_out) {
@@ -1587,25 +1709,32 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
         return fail(rc);
   }
   if (want_gram) {
-    const size_t W = (size_t)e->w;
-    if (gram && hipMemcpy2DAsync(gram, W * sizeof(double), e->d_gram, (size_t)e->ncol * sizeof(double),
-                                 W * sizeof(double), W, hipMemcpyDeviceToHost, st) != hipSuccess)
-      return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
-    if (Atb && hipMemcpyAsync(Atb, e->d_gram + W * e->ncol, W * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
-      return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
-    if (btb && hipMemcpyAsync(btb, e->d_gram + W * e->ncol + W, sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess)
+    // the whole (W+1)^2 buffer in ONE DMA into page-locked memory; gram / Atb / btb are split out on the host
+    // after the synchronize (three copies into the caller's pageable arrays cost ~50 us of staged-copy overhead)
+    if (!e->h_gram) HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_gram),
+                                             (size_t)e->ncol * e->ncol * sizeof(double), hipHostMallocDefault));
+    if (hipMemcpyAsync(e->h_gram, e->d_gram, (size_t)e->ncol * e->ncol * sizeof(double), hipMemcpyDeviceToHost, st) !=
+        hipSuccess)
       return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
   }
   tph[2] = ms_since(t0);  // + kernels and output copies enqueued
   const hipError_t sst = hipStreamSynchronize(st);
   host_unregister(e, reg);
+  stager.finish();  // every chunk packed and checked
+  if (stager.contacts_bad()) return contact_error();
+  if (sst == hipSuccess && want_gram) {
+    const size_t W = (size_t)e->w, n1 = (size_t)e->ncol;
+    if (gram)
+      for (size_t i = 0; i < W; ++i) std::memcpy(gram + i * W, e->h_gram + i * n1, W * sizeof(double));
+    if (Atb) std::memcpy(Atb, e->h_gram + W * n1, W * sizeof(double));
+    if (btb) *btb = e->h_gram[W * n1 + W];
+  }
   tph[3] = ms_since(t0);  // + synchronised
   if (trace)
-    std::fprintf(stderr, "sysid_build N=%lld flags=%u staged=%d: contacts %.3f, staging started %.3f, kernels enqueued "
-                 "%.3f, launched %.3f, done %.3f ms\n", (long long)N, flags, (int)staged, tph[0], tph[1], t_kern, tph[2],
-                 tph[3]);
+    std::fprintf(stderr, "sysid_build N=%lld flags=%u: contacts %.3f, staging started %.3f, kernels enqueued "
+                 "%.3f, launched %.3f, done %.3f ms\n", (long long)N, flags, tph[0], tph[1], t_kern, tph[2], tph[3]);
   if (trace && !stager.stamps().empty()) {
-    std::string line = "  chunk stamps (packed, DMA enqueued) ms:";
+    std::string line = "  chunk stamps (packed, DMA + K0W enqueued) ms:";
     char buf[32];
     for (double x : stager.stamps()) {
       std::snprintf(buf, sizeof buf, " %.3f", x);
@@ -1615,6 +1744,31 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
   }
   if (sst != hipSuccess) return set_err(e, SYSID_E_DEVICE, "stream sync failed: %s", hipGetErrorString(sst));
   return SYSID_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const double* ddq, const double* tau,
+                    const double* cnt, int64_t N, int64_t ld, uint32_t flags, double* Y_proj, double* tau_proj,
+                    double* B_v, double* B_c, double* gram, double* Atb, double* btb) {
+  const HostInputs in{q, 8, dq, ddq, tau, cnt, 8, ld};
+  return build_host(e, in, N, flags, Y_proj, tau_proj, B_v, B_c, gram, Atb, btb);
+}
+
+int32_t sysid_check_contacts(const sysid_engine* e, const double* cnt, int64_t N, int64_t ld, int64_t* bad) {
+  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
+  if (e->nc == 0 || N <= 0) return SYSID_OK;
+  if (!cnt || ld < N) return set_err(const_cast<sysid_engine*>(e), SYSID_E_INVALID, "bad contact buffer");
+  return check_contacts_t(const_cast<sysid_engine*>(e), cnt, N, ld, bad);
+}
+
+int32_t sysid_build_f32qc(sysid_engine* e, const float* q, const double* dq, const double* ddq, const double* tau,
+                          const float* cnt, int64_t N, int64_t ld, uint32_t flags, double* Y_proj, double* tau_proj,
+                          double* B_v, double* B_c, double* gram, double* Atb, double* btb) {
+  const HostInputs in{q, 4, dq, ddq, tau, cnt, 4, ld};
+  return build_host(e, in, N, flags, Y_proj, tau_proj, B_v, B_c, gram, Atb, btb);
 }
 
 // ---- diagnostics --------------------------------------------------------------------------------

@@ -748,11 +748,55 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       }
     }
     wsync();
-    // Poses level by level (a joint's parent is one level up); level 1 is final after the placement pass.
-    for (int lvl = 2; lvl <= kp.maxdepth; ++lvl) {
-      for (int j = 1 + hl; j < NJ; j += HW)
-        if (depth[j] == lvl) pose_step(j);
+    if constexpr (SPW == 1 || NVC == 18) {
+      // Every joint has its own lane (one-sample waves: NJ <= 64; the quadruped kernel: nb <= 16 of 32 lanes): each
+      // lane forms its joint's pose as the product
+      // of the placements along its revolute chain, root first — the same products in the same order as the level
+      // passes below, without their ordering point and LDS round trip per level (G1: 10 levels; Spot K1 -1.5%,
+      // profiles/r05_s4).  The results are written after one ordering point (every lane has read the placements
+      // it needs).
+      static_assert(SPW == 1 || HW >= 17, "one lane per body of the quadruped kernel (nb <= 16)");
+      const int j = 1 + hl;
+      double M[12];
+#pragma unroll
+      for (int x = 0; x < 12; ++x) M[x] = 0.0;
+      if (j < NJ && jtype[j] != JT_FREEFLYER) {
+        const int cl = chain_len[j];
+        const int* ch = chain + j * kp.maxch;
+        const double* b0 = body + BODY_STRIDE * dof_joint[ch[0]];
+#pragma unroll
+        for (int x = 0; x < 12; ++x) M[x] = b0[x];
+#pragma unroll
+        for (int t = 1; t < MAXCH; ++t) {
+          if (t >= kp.maxdepth) break;  // wave-uniform bound (chains are shorter than the tree is deep)
+          if (t < cl) {
+            const double* bl = body + BODY_STRIDE * dof_joint[ch[t]];
+            double liR[9], lit[3], R[9], tt[3];
+#pragma unroll
+            for (int x = 0; x < 9; ++x) liR[x] = bl[x];
+            lit[0] = bl[9]; lit[1] = bl[10]; lit[2] = bl[11];
+            mat3mul(M, liR, R);
+            mat3vec(M, lit, tt);
+#pragma unroll
+            for (int x = 0; x < 9; ++x) M[x] = R[x];
+            M[9] = tt[0] + M[9]; M[10] = tt[1] + M[10]; M[11] = tt[2] + M[11];
+          }
+        }
+      }
+      wsync();  // every placement read
+      if (j < NJ && jtype[j] != JT_FREEFLYER) {
+        double* bj = body + BODY_STRIDE * j;
+#pragma unroll
+        for (int x = 0; x < 12; ++x) bj[x] = M[x];
+      }
       wsync();
+    } else {
+      // Poses level by level (a joint's parent is one level up); level 1 is final after the placement pass.
+      for (int lvl = 2; lvl <= kp.maxdepth; ++lvl) {
+        for (int j = 1 + hl; j < NJ; j += HW)
+          if (depth[j] == lvl) pose_step(j);
+        wsync();
+      }
     }
 
     // ---- world motion axes of every dof; contact points ----
@@ -1236,10 +1280,16 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     // Q-form: tp = S^T tau - Qᵀ u, u_j = Q_j · S^T tau (u in the dead row-norm slots)
     if constexpr (QF) {
       if (!kp.full) {
-        for (int j = hl; j < k; j += HW) {
+        // u_j = Q_j . S^T tau: eight lanes per row j (k <= K1_QF_KMAX <= 8 rows, whole 8-lane groups active), each
+        // summing every eighth joint, then a DPP sum over the group — not one lane per row walking all nj joints
+        // (a 29-long chain of dependent LDS reads on G1)
+        static_assert(K1_QF_KMAX <= 8, "one 8-lane group per Q row");
+        const int j = hl >> 3, part = hl & 7;
+        if (j < k) {
           double acc = 0.0;
-          for (int jj = 0; jj < nja; ++jj) acc += Jc[j * nv + bd + jj] * tau[jj];
-          Ms[j] = acc;
+          for (int jj = part; jj < nja; jj += 8) acc += Jc[j * nv + bd + jj] * tau[jj];
+          acc = group_sum(acc, 8);
+          if (part == 0) Ms[j] = acc;
         }
         wsync();
       }
@@ -1550,20 +1600,36 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         }
         OutT* oi = out + 10 * (i - 1) + 4 * h;
         const double* jrs = Jws + c3;
+        // The row loops read row r + 1's Q entries and motion-axis components while row r is multiplied (one LDS
+        // wait per row, behind a row of arithmetic, instead of two waits up front), and store through the same
+        // three instructions in both lanes of a pair (an h = 0 lane rewrites its columns 2, 3 with the third
+        // store: no exec-masked branch per row).
         auto rows = [&](auto kqc) {
           constexpr int KQ = decltype(kqc)::value;
+          constexpr int KQ2 = (KQ + 1) / 2;
+          double qn[2 * KQ2], jn[3];
+          auto row_ld = [&](int r, double* qv, double* jv) {
+            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
+#pragma unroll
+            for (int j = 0; j < KQ2; ++j) {
+              const double2 v = q2[j];
+              qv[2 * j] = v.x;
+              qv[2 * j + 1] = v.y;
+            }
+            const double* jr = jrs + 6 * r;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) jv[c] = jr[c];
+          };
+          row_ld(0, qn, jn);
 #pragma unroll 1
           for (int r = 0; r < nrows; ++r) {
             const double sf = ((smask >> r) & 1ull) ? 1.0 : 0.0;
-            const double* jr = jrs + 6 * r;
-            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
-            double qr[K1_QF_KMAX];
+            double qr[2 * KQ2], jr[3];
 #pragma unroll
-            for (int j = 0; j < (KQ + 1) / 2; ++j) {
-              const double2 v = q2[j];
-              qr[2 * j] = v.x;
-              qr[2 * j + 1] = v.y;
-            }
+            for (int j = 0; j < 2 * KQ2; ++j) qr[j] = qn[j];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) jr[c] = jn[c];
+            row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
             double G[6];
 #pragma unroll
             for (int c = 0; c < 3; ++c) G[c] = sf * jr[c];
@@ -1584,7 +1650,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             OutT* o2 = oi + (int64_t)r * ldp;
             panel_store(o2, y[0], y[1]);
             panel_store(o2 + 2, y[2], y[3]);
-            if (h) panel_store(o2 + 4, y[4], y[5]);
+            panel_store(o2 + (h ? 4 : 2), h ? y[4] : y[2], h ? y[5] : y[3]);
           }
         };
         // bf16 chunk panels (the Gram-only bf16 Gram, config 5): the same row loop in f32 with packed FMAs
@@ -1606,14 +1672,24 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
           for (int pp = 0; pp < 3; ++pp)
 #pragma unroll
             for (int q = 0; q < 6; ++q) Fp[pp][q] = f32x2_t{(float)F6[2 * pp][q], (float)F6[2 * pp + 1][q]};
+          float qn[K1_QF_KMAX], jn[3];
+          auto row_ld = [&](int r, float* qv, float* jv) {
+            const float* qrow = q32 + 14 * r;
+#pragma unroll
+            for (int j = 0; j < K1_QF_KMAX; ++j) qv[j] = qrow[j];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) jv[c] = qrow[8 + c3 + c];
+          };
+          row_ld(0, qn, jn);
 #pragma unroll 1
           for (int r = 0; r < nrows; ++r) {
             const float sf = ((smask >> r) & 1ull) ? 1.0f : 0.0f;
-            const float* qrow = q32 + 14 * r;
-            float qr[K1_QF_KMAX];
+            float qr[K1_QF_KMAX], jr[3];
 #pragma unroll
-            for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = qrow[j];
-            const float* jr = qrow + 8 + c3;
+            for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = qn[j];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) jr[c] = jn[c];
+            row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
             f32x2_t g01 = f32x2_t{sf * jr[0], sf * jr[1]};
             float g2 = sf * jr[2];
 #pragma unroll
@@ -1634,7 +1710,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             __bf16* o2 = reinterpret_cast<__bf16*>(oi + (int64_t)r * ldp);
             panel_store_f32(o2, y01.x, y01.y);
             panel_store_f32(o2 + 2, y23.x, y23.y);
-            if (h) panel_store_f32(o2 + 4, y45.x, y45.y);
+            panel_store_f32(o2 + (h ? 4 : 2), h ? y45.x : y23.x, h ? y45.y : y23.y);
           }
         };
         if constexpr (std::is_same_v<OutT, __bf16>) {
@@ -1730,6 +1806,26 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pe[u] * sc[u] : (tcol[u] ? t : 0.0);
             panel_store(po, v2[0], v2[1]);
           }
+          }
+        } else if (NVC == 18 && HW == 32 && !CMP && NG == 2) {
+          // Spot / Solo (13 column pairs: two 16-lane groups, 9 rows each): every row's LDS reads issued up front
+          // instead of one wait per row of the rolled loop (Spot K1 -4%, profiles/r05_s4)
+          constexpr int NR = NVC > 0 ? NVC / 2 : 1;
+          double pv[NR][2], tv[NR];
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            const int r = fg + 2 * i;
+            const double* pr = Ps + r * NVC + bd;
+            pv[i][0] = pr[jc[0]];
+            pv[i][1] = pr[jc[1]];
+            tv[i] = tps[r];
+          }
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            double v2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pv[i][u] * sc[u] : (tcol[u] ? tv[i] : 0.0);
+            panel_store(po + i * pstep, v2[0], v2[1]);
           }
         } else {
           for (int r = fg; r < nrows; r += NG, po += pstep) {
@@ -2024,6 +2120,32 @@ __device__ __forceinline__ int k1s_wave_incl(int v, int lane) {  // inclusive sc
 // came back NaN or empty; tools/dbg_ns_graph.py, profiles/r04_dbg).  Kernel nodes are ordered.
 __global__ void __launch_bounds__(256) k0_zero_u64(unsigned long long* __restrict__ p, int64_t n) {
   for (int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) p[x] = 0ull;
+}
+
+// Host entry points' wire format (sysid_engine.hip, wire_layout): one block per staged chunk of n samples — q rows
+// (nq x n, float32 when the caller's q is float32 as read_data returns it, else float64), the dq / ddq / tau rows
+// (nd x n float64) and the contact rows (nc x n bytes: 1 where the value is non-zero, the only property the
+// projector reads) — sent as one DMA.  K0W widens chunk [c0, c0 + n) into the row-major float64 input block K1
+// reads (rows x ld) and zeroes K1's claim counters (`work`, nwork words) on the way: one launch per chunk, exact
+// (float32 -> float64 and the 0 / 1 contacts).  Block (x, y): samples of row y.
+__global__ void __launch_bounds__(256) k0_widen(const unsigned char* __restrict__ wire, int64_t n, int nq, int nd,
+                                                int qsz, int64_t offd, int64_t offc, double* __restrict__ dst,
+                                                int64_t ld, unsigned long long* __restrict__ work, int nwork) {
+  if (work != nullptr && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int x = threadIdx.x; x < nwork; x += 256) work[x] = 0ull;
+  const int r = blockIdx.y;
+  double* out = dst + (int64_t)r * ld;
+  for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n; s += (int64_t)gridDim.x * 256) {
+    double v;
+    if (r < nq)
+      v = qsz == 4 ? (double)reinterpret_cast<const float*>(wire)[(int64_t)r * n + s]
+                   : reinterpret_cast<const double*>(wire)[(int64_t)r * n + s];
+    else if (r < nq + nd)
+      v = reinterpret_cast<const double*>(wire + offd)[(int64_t)(r - nq) * n + s];
+    else
+      v = wire[offc + (int64_t)(r - nq - nd) * n + s] ? 1.0 : 0.0;
+    out[s] = v;
+  }
 }
 
 __global__ void __launch_bounds__(256)

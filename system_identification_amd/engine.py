@@ -38,6 +38,7 @@ LIB_PATH = os.environ.get("SYSID_LIB") or os.path.join(os.path.dirname(os.path.a
 _c = ctypes
 _dp = _c.POINTER(_c.c_double)
 _vp = _c.c_void_p
+_fp = _c.POINTER(_c.c_float)
 SIGNATURES = [
     ("sysid_abi_version", _c.c_int32, []),
     ("sysid_model_create", _c.c_int32, [_vp, _c.c_size_t, _c.c_int32, _c.POINTER(_vp)]),
@@ -46,6 +47,8 @@ SIGNATURES = [
     ("sysid_dims", _c.c_int32, [_vp] + [_c.POINTER(_c.c_int32)] * 7),
     ("sysid_build", _c.c_int32, [_vp, _dp, _dp, _dp, _dp, _dp, _c.c_int64, _c.c_int64, _c.c_uint32,
                                  _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    ("sysid_build_f32qc", _c.c_int32, [_vp, _fp, _dp, _dp, _dp, _fp, _c.c_int64, _c.c_int64, _c.c_uint32,
+                                       _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
     ("sysid_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64, _c.c_uint32]),
     ("sysid_build_device", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64,
                                         _vp, _vp, _c.c_size_t, _vp]),
@@ -199,11 +202,15 @@ class Engine:
 
     # ---- host-buffer path --------------------------------------------------------------------
     def build(self, q, dq, ddq, tau, cnt, flags: int = EMIT_ALL) -> dict:
-        """Channel-major (channels x N) inputs -> stacked outputs (+ Gram), all float64 numpy."""
+        """Channel-major (channels x N) inputs -> stacked outputs (+ Gram), all float64 numpy.  q and contact as
+        float32 arrays (what read_data returns, demo/spot_identification.py:10-14) go to sysid_build_f32qc and
+        travel to the device as float32 / contact flags; otherwise everything is float64 (sysid_build)."""
+        f32 = getattr(q, "dtype", None) == np.float32 and getattr(cnt, "dtype", None) == np.float32
         ins = []
         for a, rows, name in ((q, self.nq, "q"), (dq, self.nv, "dq"), (ddq, self.nv, "ddq"),
                               (tau, self.nj, "tau"), (cnt, self.n_contact, "contact")):
-            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+            wide = not (f32 and name in ("q", "contact"))
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64 if wide else np.float32))
             if a.ndim == 1:
                 a = a.reshape(-1, 1)
             if a.shape[0] != rows:
@@ -222,8 +229,14 @@ class Engine:
         G = np.empty((self.w, self.w)) if flags & EMIT_GRAM else None
         g = np.empty(self.w) if flags & EMIT_GRAM else None
         btb = np.zeros(1) if flags & EMIT_GRAM else None
-        rc = self.lib.sysid_build(self._h, *[_ptr(a) for a in ins], N, N, int(flags),
-                                  _ptr(Y), _ptr(t), _ptr(Bv), _ptr(Bc), _ptr(G), _ptr(g), _ptr(btb))
+        if f32:
+            fp = lambda a: a.ctypes.data_as(_fp)  # noqa: E731
+            rc = self.lib.sysid_build_f32qc(self._h, fp(ins[0]), _ptr(ins[1]), _ptr(ins[2]), _ptr(ins[3]), fp(ins[4]),
+                                            N, N, int(flags), _ptr(Y), _ptr(t), _ptr(Bv), _ptr(Bc), _ptr(G), _ptr(g),
+                                            _ptr(btb))
+        else:
+            rc = self.lib.sysid_build(self._h, *[_ptr(a) for a in ins], N, N, int(flags),
+                                      _ptr(Y), _ptr(t), _ptr(Bv), _ptr(Bc), _ptr(G), _ptr(g), _ptr(btb))
         self._check(rc)
         if Y is not None:
             out["Y_proj"] = Y

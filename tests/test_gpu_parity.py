@@ -153,6 +153,29 @@ def test_contact_contract_and_shape_errors():
         eng("spot").build(d["q"][:5], d["dq"], d["ddq"], d["tau"], d["contact"], EMIT_ALL)
 
 
+@pytest.mark.parametrize("flags", [EMIT_ALL, EMIT_GRAM])
+@pytest.mark.parametrize("f32", [False, True])
+def test_contact_contract_checked_while_staging(flags, f32):
+    """The host entry points check the contact contract in their packing threads, chunk by chunk (Stager::check):
+    a violation in the last staged chunk still fails the call before any output is written, and the message names
+    the first offending sample; the same inputs without the violations build normally afterwards."""
+    model = load_robot("spot")
+    e = eng("spot")
+    N = 20001
+    d = generate(model, N, config_index=1)
+    cnt = d["contact"].copy()
+    cnt[:, 19000] = [0.5, 0.0, 0.0, 0.0]
+    cnt[:, 15000] = [0.0, 0.5, 0.0, 0.0]
+    q = d["q"].astype(np.float32) if f32 else d["q"]
+    c = cnt.astype(np.float32) if f32 else cnt
+    with pytest.raises(ValueError, match="sample 15000"):
+        e.build(q, d["dq"], d["ddq"], d["tau"], c, flags)
+    ok = e.build(q, d["dq"], d["ddq"], d["tau"], d["contact"].astype(c.dtype), flags)
+    ref_out = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], flags)
+    for k in ok:
+        assert np.array_equal(np.asarray(ok[k]), np.asarray(ref_out[k])), k
+
+
 def test_device_api_views_and_determinism():
     import torch
     model = load_robot("spot")
@@ -333,11 +356,11 @@ def test_gram_only_chunked(robot, N):
                                                     ("spot", 40000, 0, 64 << 20),
                                                     ("g1_29dof", 9001, 0, 0)])
 def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
-    """Host Gram-only entry point with its inputs staged in `chunks` chunk-major blocks (each chunk packed as its
-    own block and sent as one DMA, its K1 reading it with ld = the chunk's length), ragged last chunk, and staged
-    chunks larger than the workspace's panel chunk (ws_chunk bytes: several K1 launches per staged block): the same
-    normal equations as the device entry point on the row-major block, to rounding.  chunks = 0: the default bounds
-    (a first chunk of one K1 round, then two chunks of whole rounds)."""
+    """Host Gram-only entry point with its inputs staged in `chunks` wire blocks (each chunk packed as its own block,
+    sent as one DMA and widened by K0W into the row-major block its K1 reads), ragged last chunk, and staged chunks
+    larger than the workspace's panel chunk (ws_chunk bytes: several K1 launches per staged block): the same normal
+    equations as the device entry point on the row-major block, to rounding.  chunks = 0: the default bounds (a
+    first chunk of one K1 round, then two chunks of whole rounds)."""
     import torch
     if chunks:
         monkeypatch.setenv("SYSID_STAGE_CHUNKS", str(chunks))
@@ -359,6 +382,26 @@ def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
     assert rel(only["Atb"], G[:W, W]) < 1e-12
     assert abs(only["btb"] - G[W, W]) <= 1e-12 * abs(G[W, W])
     assert only["num_rows"] == N * model.nv
+
+
+@pytest.mark.parametrize("robot,N", [("spot", 20001), ("g1_29dof", 3001), ("solo12", 7), ("spot", 1)])
+def test_float32_q_contact_entry_point_is_bitwise_the_float64_one(robot, N):
+    """sysid_build_f32qc (q and contact in float32, as read_data returns them, demo/spot_identification.py:10-14)
+    against sysid_build on the same values in float64: the float32 -> float64 widening is exact and the contact
+    bytes carry the non-zero test K1 applies (values 2 = LOST included), so every output is bitwise equal, stacked
+    and Gram-only, large (staged chunks) and small (one inline-packed chunk)."""
+    model = load_robot(robot)
+    e = Engine(model)
+    d = generate(model, N, config_index=7)
+    assert np.any(d["contact"] == 2.0) or N < 100
+    q32, c32 = d["q"].astype(np.float32), d["contact"].astype(np.float32)
+    assert np.array_equal(q32.astype(np.float64), d["q"]) and np.array_equal(c32.astype(np.float64), d["contact"])
+    for flags in (EMIT_ALL, EMIT_GRAM):
+        a = e.build(d["q"], d["dq"], d["ddq"], d["tau"], d["contact"], flags)
+        b = e.build(q32, d["dq"], d["ddq"], d["tau"], c32, flags)
+        assert set(a) == set(b)
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (flags, k)
 
 
 @pytest.mark.parametrize("robot,N", [("spot", 3000), ("g1_29dof", 700)])
