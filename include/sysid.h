@@ -166,7 +166,9 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
  * sysid_gram_workspace_bytes reports follows it.  That workspace is exactly: 1 KiB of K1 sample counters, the
  * chunk panel (min(chunk bytes, N·nv rows of the Gram's element type)), the split-K slabs (K2 workgroups x
  * Gram tile slots x 2 KiB: Spot <= 29 MB, G1 <= 141 MB) and, for the nullspace rows, 4·(nv + 1) bytes per
- * chunk sample of row counts and row list plus 4 bytes per 1024 samples of segment sums.  Fewer, larger chunks
+ * chunk sample of row counts and row list plus 4 bytes per 1024 samples of segment sums; while the fused kernel is
+ * on (sysid_set_fusion, quadrupeds, f64) at least its rings (~140 MB) and slabs.  A workspace sized before a change
+ * of these settings is checked again at launch (SYSID_E_INVALID when short, never overrun).  Fewer, larger chunks
  * are faster (each costs a K1 launch tail and a pass over the split-K slabs: 16 GiB is 2-3% faster than 4 GiB
  * on G1 1M); a smaller chunk bounds the device memory of very large N. */
 int32_t sysid_set_gram_chunk_bytes(sysid_engine* e, uint64_t bytes);
@@ -257,7 +259,9 @@ int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
  * standalone occupancy (both are register-bound at two waves per SIMD), so the fused launch measured slower than
  * K1 -> K2 -> K3 (Spot 20k: 0.445 vs 0.37 ms).  sysid_set_fusion (or SYSID_FUSE=1 at engine creation) turns
  * it on; sysid_fused tells whether `flags` run fused (with a stacked-output flag: sysid_build_device; without:
- * sysid_build_gram_device). */
+ * sysid_build_gram_device).  Every wait between the two roles is bounded (~1 s): a wave that gives up sets its
+ * workgroup's abort word, the Gram waves then write NaN tiles and later waits return at once, so a defect shows
+ * in the Gram instead of hanging the device. */
 int32_t sysid_set_fusion(sysid_engine* e, int32_t on);
 int32_t sysid_fused(const sysid_engine* e, uint32_t flags);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */

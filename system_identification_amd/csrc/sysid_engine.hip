@@ -489,7 +489,9 @@ size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
   const int64_t C = gram_chunk(e, N, prec), rows = C * e->nv;
   const size_t chunked = WORK_BYTES + cmp_head_bytes(C) + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) +
                          slab_bytes(e, rows, prec) + cmp_tail_bytes(e, C);
-  return prec == 0 && e->k12_ok ? std::max(chunked, k12_ring_ws_bytes(e, N)) : chunked;
+  // the fused ring form's rings only while fusion is on (sysid_set_fusion): a workspace sized before the fusion is
+  // switched on is refused at launch (gram_ws_bytes_prec is checked there), never overrun
+  return prec == 0 && e->k12_ok && e->fuse ? std::max(chunked, k12_ring_ws_bytes(e, N)) : chunked;
 }
 
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
@@ -1006,7 +1008,10 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     ii[MI.idx_v + j] = idx_v[j];
     ii[MI.depth + j] = depth[j];
     ii[MI.chain_len + j] = (int)chains[j].size();
-    for (size_t t = 0; t < chains[j].size(); ++t) ii[MI.chain + j * maxch_tpl + (int)t] = chains[j][t];
+    for (size_t t = 0; t < chains[j].size(); ++t) {
+      ii[MI.chain + j * maxch_tpl + (int)t] = chains[j][t];
+      ii[MI.anc + j * maxch_tpl + (int)t] = dof_joint[chains[j][t]];
+    }
     for (int k = 0; k < 3; ++k) { dd[MI.axis + 3 * j + k] = ax[3 * j + k]; dd[MI.t0 + 3 * j + k] = t0[3 * j + k]; }
     for (int k = 0; k < 9; ++k) dd[MI.R0 + 9 * j + k] = R0[9 * j + k];
   }
@@ -1051,7 +1056,13 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.has_ff = nff; kp.ff0 = ff0; kp.mimg_dbl = MI.ndbl; kp.wave_dbl = WL0.total; kp.out_cols = e->ldp;
   kp.rg = k1_row_groups(NJ, 64);  // per launch: k1_row_groups(NJ, lanes per sample)
   kp.thr_rel = 1e-14;  // rank cut of the Gram-Schmidt projector (pinv: 1e-15 sigma_max)
+  kp.thr_rel2 = kp.thr_rel * kp.thr_rel;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
+  kp.k12_spin_log2 = 23;   // the fused kernel's wait bound (~1 s)
+  kp.k12_stall_polls = 0;
+  // tests only: a short wait bound and held-back Gram waves exercise the fused kernel's give-up path
+  if (const char* v = std::getenv("SYSID_K12_SPIN_LOG2")) kp.k12_spin_log2 = std::max(1, std::min(23, std::atoi(v)));
+  if (const char* v = std::getenv("SYSID_K12_STALL_POLLS")) kp.k12_stall_polls = std::max(0, std::atoi(v));
   e->k1_maxch_tpl = maxch_tpl;
 
   // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
@@ -1262,7 +1273,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     // the fused K1 + Gram kernel: the quadruped K1 beside the 10-column Gram waves, one workgroup per CU
     if (e->k1m[0].variant == K1_C4_NV18 && e->ntc == K12_NTC) {
       const size_t lds = (size_t)(MI.ndbl + K1_WAVES * k1_spw(K1_C4_NV18) * e->k1m[0].wave_dbl) * sizeof(double) +
-                         2 * K1_WAVES * sizeof(int);  // + the ready / consumed counters
+                         (2 * K1_WAVES + 2) * sizeof(int);  // + the ready / consumed counters, the abort word
       int nb = 0;
       if (lds <= 160 * 1024 &&
           hipFuncSetAttribute(sysid_launch::k12_fn(0), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&

@@ -31,7 +31,7 @@ constexpr int K12_GW = 4;              // Gram waves per fused K1 + Gram workgro
 // Compact model image kept in LDS by every K1 workgroup.  Int section offsets are in 4-byte words,
 // double section offsets in doubles from the image start.
 struct MImg {
-  int parent, jtype, idx_q, idx_v, depth, chain_len, chain, dof_joint, dof_k, cjoint, csupp, nint;
+  int parent, jtype, idx_q, idx_v, depth, chain_len, chain, anc, dof_joint, dof_k, cjoint, csupp, nint;
   int axis, R0, t0, ct, ndbl;
 };
 
@@ -45,6 +45,7 @@ __host__ __device__ inline MImg mimg_layout(int NJ, int nv, int nc, int maxch) {
   m.depth = o; o += NJ;
   m.chain_len = o; o += NJ;
   m.chain = o; o += NJ * maxch;
+  m.anc = o; o += NJ * maxch;  // the joints of `chain` (dof_joint of each entry): the chain products' placements
   m.dof_joint = o; o += nv;
   m.dof_k = o; o += nv;
   m.cjoint = o; o += nc;
@@ -155,7 +156,12 @@ struct K1Params {
   int rg;           // row groups of the regressor-column phase (lanes = bodies x rg)
   int pov;          // 1: P overlays the projector's working set (wave_layout `pov`)
   double thr_rel;   // rank cut of the projector: remaining row norm <= thr_rel * the largest row norm
+  double thr_rel2;  // thr_rel^2, formed on the host (a kernel argument stays in SGPRs; the product hoisted out of the
+                    // sample loop took a VGPR pair, which the register-bound kernels spilled)
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
+  // the fused kernel's waits (k12_fused_panel_gram): a wait gives up after 2^k12_spin_log2 polls (~1 s at 23);
+  // k12_stall_polls > 0 (tests only) holds every Gram wave back that many polls before its first pair
+  int k12_spin_log2, k12_stall_polls;
 };
 constexpr int K1_QUAD_IN_MAX = 96;  // input channels of the quadruped K1 (nv = 18, two samples per wave)
 
@@ -500,18 +506,22 @@ constexpr int K1_CMP_KMAX = 12;
 // formed; the column phases use G_i[r] = [r in S_i] J_r - Σ_j Q_j[r] K_ij with K_ij = Σ_{d in S_i} Q_j[d] J_d
 // (S_i: the free-flyer and chain dofs of body i), k reads per row instead of a chain of P entries and axes.
 constexpr int K1_QF_KMAX = 6;
+// Register-resident Gram-Schmidt of the runtime-nv kernels: at most 8 rows (one 8-lane group each) of nv <= 8 x
+// K1_MGS_NU entries (G1: 35); larger models take the LDS form (mgs_lds)
+constexpr int K1_MGS_NU = 5;
 // K1's per-wave body, shared by the standalone K1 (k1_regressor_panel, FUSED = 0: samples claimed from device
 // counters) and the K1 waves of the fused kernel (k12_fused_panel_gram, FUSED = 1: the workgroup's sample range
 // [f0, f1) dealt statically, wave w taking steps w, w + K1_WAVES, ...; after each step's panel stores have
 // completed the wave publishes its step count in k12_ready[w] (LDS) for the Gram waves of its workgroup).
 // FUSED = 2 (the fused Gram-only mode): `panel` is the wave's ring of k12_ring steps; step t's rows go to slot
-// t % k12_ring once the Gram waves have counted (k12_consumed[w]) their loads of step t - k12_ring.
+// t % k12_ring once EVERY Gram wave has completed its loads of step t - k12_ring (k12_consumed[g] = the pairs Gram
+// wave g has finished, in order).
 template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0, int FUSED = 0>
 __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __restrict__ mimg_g,
                                         const double* __restrict__ in, int64_t N, int64_t ld,
                                         OutT* __restrict__ panel, int64_t ldp, unsigned long long* __restrict__ work,
                                         double* __restrict__ dbg, int* __restrict__ rcount, int* k12_ready,
-                                        int64_t f0, int64_t f1, const int* k12_consumed = nullptr,
+                                        int64_t f0, int64_t f1, int* k12_consumed = nullptr,
                                         int k12_ring = 0) {
   static_assert(!(POV && CMP), "the nullspace mode runs the plain layout");
   static_assert(!QF || (NVC == 0 && !POV && !CMP), "the Q-form is a runtime-nv, plain-layout kernel");
@@ -532,6 +542,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   const int* depth = mi + MI.depth;
   const int* chain_len = mi + MI.chain_len;
   const int* chain = mi + MI.chain;
+  const int* anc = mi + MI.anc;
   const int* dof_joint = mi + MI.dof_joint;
   const int* dof_k = mi + MI.dof_k;
   const int* cjoint = mi + MI.cjoint;
@@ -633,9 +644,14 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     const int64_t sh = s + half;
     // channel c of the sample at in[ib + c·is] (the row-major block: ib = sh, is = ld)
     const int64_t ib = sh, is = ld;
+    // the lane's channel offsets are recomputed per step (opaque lane index): hoisted out of the sample loop they are
+    // NXR 64-bit addresses live across every phase, and at the register limit the allocator spilled them (a scratch
+    // reload and its vmcnt(0) wait for every earlier store, once per step)
+    int hc = hl;
+    asm volatile("" : "+v"(hc));
 #pragma unroll
     for (int u = 0; u < NXR; ++u)
-      if (hl + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hl + HW * u) * is + ib];
+      if (hc + HW * u < IN && sh < N) xr[u] = in[(int64_t)(hc + HW * u) * is + ib];
   };
   double* sin_ = wr + L.in;
   const double* q = sin_;
@@ -762,15 +778,19 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       for (int x = 0; x < 12; ++x) M[x] = 0.0;
       if (j < NJ && jtype[j] != JT_FREEFLYER) {
         const int cl = chain_len[j];
-        const int* ch = chain + j * kp.maxch;
-        const double* b0 = body + BODY_STRIDE * dof_joint[ch[0]];
+        // every placement's joint up front (entries past the chain are 0, a valid slot): no dependent index load
+        // in front of each step's placement reads
+        int aj[MAXCH];
+#pragma unroll
+        for (int t = 0; t < MAXCH; ++t) aj[t] = anc[j * kp.maxch + t];
+        const double* b0 = body + BODY_STRIDE * aj[0];
 #pragma unroll
         for (int x = 0; x < 12; ++x) M[x] = b0[x];
 #pragma unroll
         for (int t = 1; t < MAXCH; ++t) {
           if (t >= kp.maxdepth) break;  // wave-uniform bound (chains are shorter than the tree is deep)
           if (t < cl) {
-            const double* bl = body + BODY_STRIDE * dof_joint[ch[t]];
+            const double* bl = body + BODY_STRIDE * aj[t];
             double liR[9], lit[3], R[9], tt[3];
 #pragma unroll
             for (int x = 0; x < 9; ++x) liR[x] = bl[x];
@@ -862,10 +882,13 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         V[0] = V[1] = V[2] = V[3] = V[4] = V[5] = A[3] = A[4] = A[5] = 0.0;
       }
       const int* ch = chain + j * kp.maxch;
+      int dch[MAXCH];  // the chain's dofs up front (unconditional: entries past the chain are 0, a valid dof)
+#pragma unroll
+      for (int t = 0; t < MAXCH; ++t) dch[t] = ch[t];
 #pragma unroll
       for (int t = 0; t < MAXCH; ++t) {  // unrolled to the compile-time chain slots (K1 -1.3%)
         if (t >= cl) break;
-        const int d = ch[t];
+        const int d = dch[t];
         const double* S = Jws + 6 * d;
         const double qd = dq[d], qdd = ddq[d];
         double Sd[6], sv[6], c1[3], c2[3], c3[3];
@@ -962,7 +985,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         {
           double nmax = 0.0;
           for (int j = 0; j < k; ++j) nmax = fmax(nmax, nrm[j]);
-          const double thr = kp.thr_rel * kp.thr_rel * nmax;
+          const double thr = kp.thr_rel2 * nmax;
           // lane pairs per row for the compile-time-nv kernel when the rows fit (uniform per sample)
           const bool pairs = NVC > 0 && NVC % 2 == 0 && 2 * k <= HW;
           // otherwise lane groups of lpr = 8, 4, 2 or 1 lanes per row, the widest whose rows fit
@@ -1040,7 +1063,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
           wsync();
           double nmax = 0.0;
           for (int jj = 0; jj < k; ++jj) nmax = fmax(nmax, nrm[jj]);
-          const double thr = kp.thr_rel * kp.thr_rel * nmax;
+          const double thr = kp.thr_rel2 * nmax;
           double sc = 0.0;  // 1/|x_j| once row j is taken; 0 if it is dropped
           for (int p = 0; p < k; ++p) {
             const double n0 = readlane_f64(myn, 2 * p), n1 = readlane_f64(myn, HW + 2 * p);
@@ -1083,6 +1106,83 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         } else {
           mgs_lds();
         }
+      } else if (8 * k <= HW && nv <= 8 * K1_MGS_NU) {
+        // Runtime-nv form for at most HW / 8 rows and nv <= 40 (G1: k <= 6, nv = 35): lane group j (8 lanes) keeps row
+        // j in registers,
+        // lane h of it the entries h, h + 8, ...; the pivot row's entries come from its group by ds_bpermute, dot
+        // products and norms are completed across the group by DPP, the norms read by readlane: no LDS round trip
+        // and no ordering point per pivot (mgs_lds keeps the rows in LDS and passes each pivot through it).
+        const int j = hl >> 3, h = hl & 7;
+        const bool row = j < k;
+        constexpr int NU = K1_MGS_NU;
+        const int nu = __builtin_amdgcn_readfirstlane((nv + 7) >> 3);  // entries per lane (<= NU)
+        double xv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int r = h + 8 * u;
+          xv[u] = u < nu && row && r < nv ? Jc[j * nv + r] : 0.0;
+        }
+        auto sqn = [&]() {
+          double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            if (u < nu) {
+              if (u & 1) a1 += xv[u] * xv[u];
+              else a0 += xv[u] * xv[u];
+            }
+          }
+          return group_sum(a0 + a1, 8);
+        };
+        double myn = sqn();  // row j's squared norm in every lane of group j
+        double nmax = 0.0;
+        for (int jj = 0; jj < k; ++jj) nmax = fmax(nmax, readlane_f64(myn, 8 * jj));
+        const double thr = kp.thr_rel2 * nmax;
+        double sc = 0.0;  // 1/|x_j| once row j is taken; 0 if it is dropped
+        bool taken = false;
+        for (int p = 0; p < k; ++p) {
+          const double best = readlane_f64(myn, 8 * p);
+          if (!(best > thr)) continue;  // dependent on the rows before it: dropped
+          const double inv = rsqrt_f64(best);
+          if (j == p) {
+            sc = inv;
+            taken = true;
+          }
+          double pv[NU];
+#pragma unroll
+          for (int u = 0; u < NU; ++u)
+            if (u < nu) pv[u] = __shfl(xv[u], 8 * p + h, 64);
+          if (row && j > p) {
+            double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+              if (u < nu) {
+                if (u & 1) c1 += pv[u] * xv[u];
+                else c0 += pv[u] * xv[u];
+              }
+            }
+            const double c = group_sum(c0 + c1, 8) * (inv * inv);
+#pragma unroll
+            for (int u = 0; u < NU; ++u)
+              if (u < nu) xv[u] -= c * pv[u];
+            myn = sqn();
+          }
+        }
+        wsync();  // every J_c read precedes the stores
+        double* Zt = wr + L.Z;
+        const int K = 3 * nc;
+        if (row) {
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            const int r = h + 8 * u;
+            if (u < nu && r < nv) {
+              const double qv = xv[u] * sc;
+              Jc[j * nv + r] = qv;
+              Zt[r * K + j] = qv;
+            }
+          }
+          if (h == 0) Ms[j] = taken ? -sc : myn;  // as mgs_lds: taken slots < 0, dropped ones their squared norm
+        }
+        wsync();
       } else {
         mgs_lds();
       }
@@ -1114,14 +1214,14 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             if constexpr (SPW == 1) return readlane_f64(v, src);
             else return __shfl(v, half * HW + src, 64);  // each half its own source lane (ds_bpermute)
           };
-          double tau[K1_CMP_KMAX];
+          // tau_a = |d_a| + 1 goes straight to nrm[a] (the taken-row flags were read into tm above, and this wave's
+          // LDS operations execute in order): no register array held across the factorisation
 #pragma unroll
           for (int a = 0; a < K1_CMP_KMAX; ++a) {
-            tau[a] = 0.0;
             if (a < rk) {
               const double d = bcast(x[a], a);
               const double rp = 1.0 / (d + (d >= 0.0 ? 1.0 : -1.0));
-              tau[a] = fabs(d) + 1.0;
+              if (hl == 0) nrm[a] = fabs(d) + 1.0;
               const double l = x[a] * rp;
 #pragma unroll
               for (int b2 = a + 1; b2 < K1_CMP_KMAX; ++b2) {
@@ -1136,11 +1236,6 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
 #pragma unroll
             for (int a = 0; a < K1_CMP_KMAX; ++a)
               if (a < rk) Jc[a * nv + hl] = x[a];
-          }
-          if (hl < rk) {
-#pragma unroll
-            for (int a = 0; a < K1_CMP_KMAX; ++a)
-              if (a == hl) nrm[a] = tau[a];
           }
           wsync();
         }
@@ -1371,12 +1466,28 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     if (steps_done > 0) publish(steps_done);
 
     if constexpr (FUSED == 2) {
-      // the ring slot this step overwrites was step steps_done - k12_ring: every Gram wave has loaded it
-      const int need = (steps_done - k12_ring + 1) * K12_GW;
-      int spins = 0;
-      while (need > 0 && __hip_atomic_load(k12_consumed + wave, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need &&
-             ++spins < (1 << 23))  // ~1 s bound: a bug must not hang the device (the Gram waves poison theirs)
-        __builtin_amdgcn_s_sleep(2);
+      // The ring slot this step overwrites held step steps_done - k12_ring, i.e. pair 4 (steps_done - k12_ring) + wave of
+      // the workgroup: EVERY Gram wave must have completed its loads of it.  Each Gram wave g counts its own finished
+      // pairs (k12_consumed[g], in pair order), and the wait is on each of them: a sum over the Gram waves (round 4)
+      // let a leading wave's count cover a lagging one that had not read the slot yet.  The wait is bounded (a bug must
+      // not hang the device): when it gives up, the workgroup's abort word (after the counters) is set before the slot
+      // is overwritten, so the Gram waves poison their tiles with NaN, and every later wait returns at once.
+      int* abort_word = k12_consumed + K12_GW;
+      const int need = (steps_done - k12_ring) * K1_WAVES + wave + 1;  // pairs every Gram wave must have finished
+      if (steps_done >= k12_ring) {
+        int spins = 0;
+        for (int g = 0; g < K12_GW; ++g) {
+          while (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
+                 __hip_atomic_load(k12_consumed + g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+            if (++spins >= (1 << kp.k12_spin_log2)) {
+              if (lane == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the abort word is in LDS before the ring store
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+      }
     }
     __builtin_amdgcn_s_setprio(0);
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
@@ -1791,16 +1902,30 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
               panel_store_f32(reinterpret_cast<__bf16*>(po), tcol[0] ? t : pe.x, tcol[1] ? t : pe.y);
             }
           } else {
+          double qn[K1_QF_KMAX], tn = 0.0;  // row r + NG's Q entries and torque, read while row r is formed
+          auto fr_ld = [&](int r) {
+            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
+#pragma unroll
+            for (int j = 0; j < K1_QF_KMAX / 2; ++j) {
+              const double2 v = q2[j];
+              qn[2 * j] = v.x;
+              qn[2 * j + 1] = v.y;
+            }
+            tn = tps[r];
+          };
+          if (fg < nrows) fr_ld(fg);
           for (int r = fg; r < nrows; r += NG, po += pstep) {
+            double qv[K1_QF_KMAX];
+#pragma unroll
+            for (int j = 0; j < K1_QF_KMAX; ++j) qv[j] = qn[j];
+            const double t = tn;
+            fr_ld(r + NG < nrows ? r + NG : r);
             double pe[2] = {r == bd + jc[0] ? 1.0 : 0.0, r == bd + jc[1] ? 1.0 : 0.0};
-            const double* qrow = Qt + r * K1_QF_KMAX;
 #pragma unroll
             for (int j = 0; j < K1_QF_KMAX; ++j) {
-              const double qr = qrow[j];
-              pe[0] -= qr * qc[j][0];
-              pe[1] -= qr * qc[j][1];
+              pe[0] -= qv[j] * qc[j][0];
+              pe[1] -= qv[j] * qc[j][1];
             }
-            const double t = tps[r];
             double v2[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) v2[u] = fcol[u] ? pe[u] * sc[u] : (tcol[u] ? t : 0.0);
@@ -1924,11 +2049,12 @@ __host__ __device__ constexpr int2 k12_tile(int slot) {
 }
 
 // RING = 0: the pairs are rows of the stacked panel; RING > 0 (fused Gram-only): pair p of the workgroup is slot
-// (p / 4) % RING of K1 wave p % 4's ring, and its loads are counted in k12_consumed[p % 4] once complete.
+// (p / 4) % RING of K1 wave p % 4's ring, and once its loads are complete k12_consumed[W] (this Gram wave's count of
+// finished pairs) becomes p + 1.
 template <int W, int NVC, int RING>
 __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, int64_t ldp, int64_t N, int64_t f0,
                                               int64_t f1, const int* k12_ready, double* __restrict__ slab,
-                                              int* k12_consumed) {
+                                              int* k12_consumed, int spin_log2, int stall_polls) {
   constexpr K12Role R = k12_role(W);
   constexpr int NB = R.col[0] + 1;         // fragment blocks 0 .. col[0] (every role's first column is its widest)
   constexpr int NT = R.ntiles;
@@ -1940,14 +2066,21 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
   bool bad = false;
+  int* abort_word = k12_consumed + K12_GW;  // set by any wave of the workgroup whose wait gave up
+  for (int x = 0; x < stall_polls; ++x) __builtin_amdgcn_s_sleep(2);  // tests: force the K1 waves' waits to expire
   // a pair is ready once its K1 wave (pair % 4) has published step pair / 4
   auto wait_pair = [&](int64_t p) {
     const int v = (int)(p & (K1_WAVES - 1)), need = (int)(p / K1_WAVES) + 1;
     int spins = 0;
     while (__hip_atomic_load(k12_ready + v, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 23)) {  // ~1 s: never expected; give up rather than hang the device
+      if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) {
         bad = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins >= (1 << spin_log2)) {  // ~1 s: never expected; give up rather than hang the device
+        bad = true;
+        if (lane == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
       }
     }
@@ -1975,8 +2108,7 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
     if constexpr (RING > 0) {
       constexpr int Y = decltype(younger)::value;
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Y) : "memory");
-      if (lane == 0) __hip_atomic_fetch_add(k12_consumed + (p & (K1_WAVES - 1)), 1, __ATOMIC_RELEASE,
-                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_store(k12_consumed + W, (int)(p + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     (void)p;
   };
@@ -2051,6 +2183,8 @@ __device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, 
     }
     consumed(p, std::integral_constant<int, 0>{});
   }
+  // a K1 wave that gave up overwrote a ring slot that may not have been read: the tiles are poisoned too
+  if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) bad = true;
   double* o = slab + ((size_t)blockIdx.x * K12_NSLOTS + R.base) * 256;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -2071,7 +2205,7 @@ k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, con
   {
     uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
     for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
-    if (threadIdx.x < 2 * K1_WAVES) ready[threadIdx.x] = 0;  // ready[4], consumed[4]
+    if (threadIdx.x < K1_WAVES + K12_GW + 1) ready[threadIdx.x] = 0;  // ready[4], consumed[4], abort word
   }
   __syncthreads();
   const int64_t P = (N + SPW - 1) / SPW;
@@ -2089,10 +2223,10 @@ k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, con
     }
   } else {
     switch (wave - K1_WAVES) {
-      case 0: k12_gram_wave<0, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
-      case 1: k12_gram_wave<1, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
-      case 2: k12_gram_wave<2, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
-      default: k12_gram_wave<3, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed); break;
+      case 0: k12_gram_wave<0, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
+      case 1: k12_gram_wave<1, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
+      case 2: k12_gram_wave<2, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
+      default: k12_gram_wave<3, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
     }
   }
 }

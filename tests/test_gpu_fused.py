@@ -171,3 +171,44 @@ def test_no_state_carried_in_the_workspace(robot, rows, fuse):
     e.build_device(din, N, EMIT_ALL, f)
     torch.cuda.synchronize()
     assert torch.equal(f["gram"], F0) and torch.equal(f["panel"][: N * e.nv], P0[: N * e.nv])
+
+
+@pytest.mark.parametrize("form", ["ring", "full"])
+def test_fused_give_up_poisons_the_gram_and_returns(form, monkeypatch):
+    """The fused kernel's waits are bounded.  With a short bound (SYSID_K12_SPIN_LOG2, a test knob read at model
+    creation) they give up: in the Gram-only ring form the K1 waves' waits for their ring slots, with the Gram waves
+    held back (SYSID_K12_STALL_POLLS); in the full-output form the Gram waves' waits for their K1 waves' steps.
+    The workgroup's abort word then makes every Gram wave write NaN tiles, later waits return at once, and the
+    launch completes promptly (a K1-side give-up used to overwrite unread ring slots silently and leave
+    later waits spinning for ~1 s each)."""
+    import time
+    import torch
+    monkeypatch.setenv("SYSID_K12_SPIN_LOG2", "8" if form == "ring" else "2")
+    monkeypatch.setenv("SYSID_K12_STALL_POLLS", "100000" if form == "ring" else "0")
+    model = load_robot("spot")
+    e = Engine(model)
+    e.set_fusion(True)
+    N = 20000
+    d = generate(model, N, config_index=7)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    t0 = time.perf_counter()
+    if form == "ring":
+        b = e.alloc_gram_device(N)
+        e.build_gram_device(din, N, b, precision="f64")
+    else:
+        b = e.alloc_device(N, EMIT_ALL)
+        e.build_device(din, N, EMIT_ALL, b)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    G = b["gram"].cpu().numpy()
+    assert np.isnan(G).any(), form
+    assert dt < 5.0, dt
+    # the same engine without the knobs' effect on a fresh model builds the right Gram again
+    monkeypatch.delenv("SYSID_K12_SPIN_LOG2")
+    monkeypatch.delenv("SYSID_K12_STALL_POLLS")
+    e2 = Engine(model)
+    e2.set_fusion(True)
+    b2 = e2.alloc_gram_device(N)
+    e2.build_gram_device(din, N, b2, precision="f64")
+    torch.cuda.synchronize()
+    assert np.all(np.isfinite(b2["gram"].cpu().numpy()))

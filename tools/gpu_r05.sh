@@ -62,6 +62,12 @@ for step in "$@"; do
       grep -v amdgpu.ids $OUT/e2e2.txt ;;
     abk1)
       bash tools/ab_rounds.sh $TAG/abk1 spot 4 tools/_libs/base.so tools/_libs/fric.so tools/_libs/fc.so || exit 1 ;;
+    ab)
+      bash tools/ab_rounds2.sh $TAG/ab ${AB_ROUNDS:-3} "${AB_WL:-spot_full spot_go g1_full g1_bf16}" $AB_LIBS || exit 1 ;;
+    ring)
+      for lib in $RING_LIBS; do
+        SYSID_LIB=$PWD/$lib timeout -k 10 120 python tools/dbg_ring.py 100001 4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/ring.txt || exit 1
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
