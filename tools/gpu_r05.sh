@@ -68,6 +68,23 @@ for step in "$@"; do
       for lib in $RING_LIBS; do
         SYSID_LIB=$PWD/$lib timeout -k 10 120 python tools/dbg_ring.py 100001 4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/ring.txt || exit 1
       done ;;
+    stagger)
+      : > $OUT/stagger.txt
+      for r in 1 2 3; do
+        for st in 0 2 4 8; do
+          SYSID_K1_STAGGER=$st SYSID_LIB=$PWD/tools/_libs/stag.so timeout -k 10 300 python tools/ab_kernels.py spot_full spot_go g1_full 2>&1 | grep "^AB " | sed "s/stag.so/stag$st/" >> $OUT/stagger.txt || exit 1
+        done
+      done
+      python - $OUT/stagger.txt <<'PY'
+import sys, statistics, collections
+rows = collections.defaultdict(list)
+for line in open(sys.argv[1]):
+    p = line.split()
+    rows[(p[1], p[2])].append(float(p[4]))
+for (lib, wl), vs in sorted(rows.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+    print("%-10s %-8s n=%d K1 median %.4f" % (wl, lib, len(vs), statistics.median(vs)))
+PY
+      ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
