@@ -68,21 +68,23 @@ for step in "$@"; do
       for lib in $RING_LIBS; do
         SYSID_LIB=$PWD/$lib timeout -k 10 120 python tools/dbg_ring.py 100001 4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/ring.txt || exit 1
       done ;;
-    stagger)
-      : > $OUT/stagger.txt
-      for r in 1 2 3; do
-        for st in 0 2 4 8; do
-          SYSID_K1_STAGGER=$st SYSID_LIB=$PWD/tools/_libs/stag.so timeout -k 10 300 python tools/ab_kernels.py spot_full spot_go g1_full 2>&1 | grep "^AB " | sed "s/stag.so/stag$st/" >> $OUT/stagger.txt || exit 1
+    envab)
+      # interleaved A/B of one library over an environment switch: ENVAB_VAR, ENVAB_VALS, ENVAB_WL, ENVAB_ROUNDS
+      : > $OUT/envab.txt
+      for r in $(seq 1 ${ENVAB_ROUNDS:-3}); do
+        for v in $ENVAB_VALS; do
+          env $ENVAB_VAR=$v timeout -k 10 300 python tools/ab_kernels.py $ENVAB_WL 2>&1 | grep "^AB " | sed "s/libsysid.so/$ENVAB_VAR=$v/" >> $OUT/envab.txt || exit 1
         done
       done
-      python - $OUT/stagger.txt <<'PY'
+      python - $OUT/envab.txt <<'PY'
 import sys, statistics, collections
 rows = collections.defaultdict(list)
 for line in open(sys.argv[1]):
     p = line.split()
-    rows[(p[1], p[2])].append(float(p[4]))
+    rows[(p[1], p[2])].append([float(p[4]), float(p[6]), float(p[8])])
 for (lib, wl), vs in sorted(rows.items(), key=lambda kv: (kv[0][1], kv[0][0])):
-    print("%-10s %-8s n=%d K1 median %.4f" % (wl, lib, len(vs), statistics.median(vs)))
+    med = [statistics.median(c) for c in zip(*vs)]
+    print("%-10s %-16s n=%d  K1 %.4f  K2 %.4f  K3 %.4f" % (wl, lib, len(vs), *med))
 PY
       ;;
     *) echo "unknown step $step"; exit 2 ;;
