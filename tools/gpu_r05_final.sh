@@ -3,15 +3,16 @@
 # Gram-only, config 4 whole; G1 20k full outputs, 125k bf16, config 5 whole in f64 / f32 / bf16), rocprofv3 kernel
 # stats of the driver-settings bench, FETCH_SIZE / WRITE_SIZE passes (pmc_summary.json, read by bench.py for
 # roofline.traffic) and SQ counter passes of the Spot headline and the G1 bf16 K1.
-# Usage: bash tools/gpu_r05_final.sh [tag] [first step]   (steps: suite bench g1 prof pmc)
+# Usage: bash tools/gpu_r05_final.sh [tag] [first step] [stop before step]   (steps: suite bench g1 prof pmc)
 set -o pipefail
 TAG=${1:-r05_final}
 FROM=${2:-suite}
+STOP=${3:-none}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 go=0
-step() { [ "$1" = "$FROM" ] && go=1; [ $go -eq 1 ]; }
+step() { [ "$1" = "$FROM" ] && go=1; [ "$1" = "$STOP" ] && go=0; [ $go -eq 1 ]; }
 if step suite; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc $rc"; grep -E " passed| failed" $OUT/pytest_gpu.log | tail -2; grep FAILED $OUT/pytest_gpu.log | head
