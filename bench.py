@@ -177,9 +177,19 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    # Dev rehearsal of the multi-rank path on a one-GPU box (SYSID_BENCH_REHEARSE=1; never the driver's runs): every
+    # rank on cuda:0 and the process group over gloo.  RCCL refuses two ranks on one GPU, so the engine's C-ABI
+    # exchange fails to come up and every rank takes the torch.distributed fallback: the rehearsal runs the
+    # orchestration (shards, barriers, max-over-ranks timing, the exchange check, rank 0's line), not RCCL.
+    rehearse = world > 1 and os.environ.get("SYSID_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from system_identification_amd.distributed import RcclGramComm, make_gram_exchange, shard_range
     from system_identification_amd.engine import EMIT_ALL, GRAM_PRECISION, GRAM_ROWS, Engine
@@ -224,6 +234,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             return int(t.item()) == 1
         comm, exchange_name = make_gram_exchange(eng, rank, world, share_id, all_ok)
+        if rehearse:
+            exchange_name = "rehearsal on one GPU over gloo: " + exchange_name
 
     if args.gram_only:
         # config 5: 16 GiB chunk panels (the library default is 4 GiB; 16 GiB measured 2-3% faster on G1 1M)
@@ -355,6 +367,12 @@ def main():
         # the packed exchange carries the row count: the job's N·nv (the Solver's 1/num_rows, solver.py:190)
         exchange_check["num_rows"] = float(xbuf[-1].item())
         exchange_check["num_rows_ok"] = exchange_check["num_rows"] == float(total_per_step * model.nv)
+    elif world > 1:  # the torch.distributed fallback: every rank must hold the same summed Gram too
+        sums = torch.stack([bufs["gram"].sum(), bufs["gram"].abs().sum()])
+        hi, lo = sums.clone(), sums.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        exchange_check = {"ranks_agree": bool(torch.equal(hi, lo)), "buffers": 1}
 
     # Labelled side figures, all after the timed region: the steady state (250 ms of untimed steps, then the same
     # K steps re-timed; rank 0 at N = 1) and the host-entry-point legs (SURVEY §8d's end-to-end rate,
