@@ -764,7 +764,44 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       }
     }
     wsync();
-    if constexpr (SPW == 1 || NVC == 18) {
+    if constexpr (SPW == 1) {
+      // One-sample waves (NJ <= 65: one lane per joint), poses by pointer jumping: lane j holds M_j, its pose in the
+      // frame of joint p_j (initially its placement liMi, p_j its parent); each pass composes M_j <- M_{p_j} M_j and
+      // jumps p_j <- p_{p_j}, every lane reading the values of the pass's start (LDS slots, pointers by ds_bpermute),
+      // until p_j is the root (the universe, or the free-flyer whose frame the poses are in).  ceil(log2(depth))
+      // passes of one 3x4 product instead of one per chain level (G1: 4 instead of up to 10); the products associate
+      // differently from the level order (rounding-level differences).
+      const int j = 1 + hl;
+      const bool jv = j < NJ;
+      auto is_root = [&](int p) { return p == 0 || jtype[p] == JT_FREEFLYER; };
+      int pj = jv ? parent[j] : 0;
+      bool done = !jv || jtype[j] == JT_FREEFLYER || is_root(pj);
+      double* bj = body + BODY_STRIDE * (jv ? j : 1);
+      double M[12];
+#pragma unroll
+      for (int x = 0; x < 12; ++x) M[x] = bj[x];
+      for (int it = 0; (1 << it) < kp.maxdepth; ++it) {
+        const double* bp = body + BODY_STRIDE * (done ? 1 : pj);
+        double Mp[12];
+#pragma unroll
+        for (int x = 0; x < 12; ++x) Mp[x] = bp[x];
+        const int pp = __shfl(pj, done ? hl : pj - 1, 64);
+        wsync();  // every lane has read the pass's poses before any is overwritten
+        if (!done) {
+          double R[9], tt[3];
+          mat3mul(Mp, M, R);
+          mat3vec(Mp, M + 9, tt);
+#pragma unroll
+          for (int x = 0; x < 9; ++x) M[x] = R[x];
+          M[9] = tt[0] + Mp[9]; M[10] = tt[1] + Mp[10]; M[11] = tt[2] + Mp[11];
+#pragma unroll
+          for (int x = 0; x < 12; ++x) bj[x] = M[x];
+          pj = pp;
+          done = is_root(pj);
+        }
+        wsync();
+      }
+    } else if constexpr (NVC == 18) {
       // Every joint has its own lane (one-sample waves: NJ <= 64; the quadruped kernel: nb <= 16 of 32 lanes): each
       // lane forms its joint's pose as the product
       // of the placements along its revolute chain, root first — the same products in the same order as the level
