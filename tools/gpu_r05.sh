@@ -68,6 +68,16 @@ for step in "$@"; do
       for lib in $RING_LIBS; do
         SYSID_LIB=$PWD/$lib timeout -k 10 120 python tools/dbg_ring.py 100001 4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/ring.txt || exit 1
       done ;;
+    e2erows)
+      : > $OUT/e2e_rows.txt
+      for r in 1 2 3; do
+        for rows in nullspace projector; do
+          timeout -k 10 120 python tools/e2e_time.py spot 20000 12 f32 gram $rows >> $OUT/e2e_rows.txt 2>&1 || { echo "e2e rows failed"; tail $OUT/e2e_rows.txt; exit 1; }
+        done
+      done
+      timeout -k 10 200 python bench.py --gram-only --rows projector --no-cpu-baseline --no-e2e --steps 20 --warmup 5 > $OUT/bench_go_projector.json 2>/dev/null || exit 1
+      timeout -k 10 200 python bench.py --gram-only --rows nullspace --no-cpu-baseline --no-e2e --steps 20 --warmup 5 > $OUT/bench_go_nullspace.json 2>/dev/null || exit 1
+      grep -v amdgpu.ids $OUT/e2e_rows.txt; python tools/bench_summary.py $OUT/bench_go_projector.json $OUT/bench_go_nullspace.json ;;
     envab)
       # interleaved A/B of one library over an environment switch: ENVAB_VAR, ENVAB_VALS, ENVAB_WL, ENVAB_ROUNDS
       : > $OUT/envab.txt
