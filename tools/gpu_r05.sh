@@ -68,6 +68,14 @@ for step in "$@"; do
       for lib in $RING_LIBS; do
         SYSID_LIB=$PWD/$lib timeout -k 10 120 python tools/dbg_ring.py 100001 4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/ring.txt || exit 1
       done ;;
+    e2esplit)
+      : > $OUT/e2e_split.txt
+      for r in 1 2 3; do
+        for b in 4096 6144 8192 10240; do
+          SYSID_STAGE_BOUNDS=$b timeout -k 10 120 python tools/e2e_time.py spot 20000 12 f32 gram >> $OUT/e2e_split.txt 2>&1 || { echo "e2e split failed"; tail $OUT/e2e_split.txt; exit 1; }
+        done
+      done
+      grep -v amdgpu.ids $OUT/e2e_split.txt ;;
     e2erows)
       : > $OUT/e2e_rows.txt
       for r in 1 2 3; do
