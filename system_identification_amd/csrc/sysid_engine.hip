@@ -1614,11 +1614,13 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
                          ((flags & SYSID_EMIT_FRICTION) && (B_v || B_c) && e->nj);
   const bool gram_only = want_gram && !panel_out;
   const int gp = gram_prec(flags);
-  // Gram-only staged chunks on K1's round boundaries (SYSID_STAGE_CHUNKS=k: k equal chunks instead).
-  // Two staged chunks: a first chunk of one K1 round (every resident wave one step: its DMA is short, so the kernels
-  // start early), then the rest (Spot 20k Gram-only e2e, float32 q: 0.548-0.556 ms best of 12 against 0.561-0.576 for
-  // one round + two halves of whole rounds, 0.625-0.642 for three round-aligned chunks after the first, 0.642 for one
-  // chunk; profiles/r05_s4).  SYSID_STAGE_SPLIT=3: the one-round chunk, then two chunks of whole rounds.
+  // Gram-only staged chunks (SYSID_STAGE_CHUNKS=k: k equal chunks instead).  Two staged chunks: a short first one,
+  // whose DMA lands early so the kernels start while the second chunk's DMA runs, then the rest (against three or more
+  // chunks, which each add a K1 tail, a row list and a K2 pass to the kernel chain: profiles/r05_s4).  The first chunk
+  // is ~30% of N in half K1 rounds (a round = every resident wave one step), at least one round: Spot 20k Gram-only
+  // e2e, float32 q, 5 interleaved rounds of 12 calls: first chunk 4,096 / 5,120 / 6,144 / 7,168 samples, median
+  // 0.556 / 0.530 / 0.526 / 0.532 ms, best 0.530 / 0.514 / 0.499 / 0.509 (profiles/r05_s24).
+  // SYSID_STAGE_SPLIT=3: a one-round chunk, then two chunks of whole rounds.
   std::vector<int64_t> round_bounds;
   const bool big = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20);
   if (gram_only && big) {
@@ -1631,7 +1633,9 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
       const int64_t mid = R + ((N - R + 2 * R - 1) / (2 * R)) * R;  // whole rounds, the larger half first
       round_bounds = {0, R, std::min(mid, N - 1), N};
     } else if (R > 0 && N >= 2 * R) {
-      round_bounds = {0, R, N};
+      const int64_t half = std::max<int64_t>(1, R / 2);
+      const int64_t first = std::min(std::max((3 * N / 10 + half - 1) / half * half, R), N - R);
+      round_bounds = {0, first, N};
     } else {
       round_bounds = {0, (N + 1) / 2, N};
     }
