@@ -70,12 +70,32 @@ for step in "$@"; do
       done ;;
     e2esplit)
       : > $OUT/e2e_split.txt
-      for r in 1 2 3; do
-        for b in 4096 6144 8192 10240; do
+      for r in $(seq 1 ${E2E_ROUNDS:-3}); do
+        for b in ${E2E_BOUNDS:-4096 6144 8192 10240}; do
           SYSID_STAGE_BOUNDS=$b timeout -k 10 120 python tools/e2e_time.py spot 20000 12 f32 gram >> $OUT/e2e_split.txt 2>&1 || { echo "e2e split failed"; tail $OUT/e2e_split.txt; exit 1; }
         done
       done
       grep -v amdgpu.ids $OUT/e2e_split.txt ;;
+    e2eenv)
+      # host e2e over an environment switch: E2E_VAR, E2E_VALS, E2E_ROUNDS
+      : > $OUT/e2e_env.txt
+      for r in $(seq 1 ${E2E_ROUNDS:-5}); do
+        for v in $E2E_VALS; do
+          env $E2E_VAR=$v timeout -k 10 120 python tools/e2e_time.py spot 20000 12 f32 gram 2>&1 | grep -v amdgpu.ids | sed "s/^/$E2E_VAR=$v /" >> $OUT/e2e_env.txt || { echo "e2e env failed"; tail $OUT/e2e_env.txt; exit 1; }
+        done
+      done
+      python - $OUT/e2e_env.txt <<'PY'
+import re, sys, statistics, collections
+rows = collections.defaultdict(lambda: ([], []))
+for l in open(sys.argv[1]):
+    m = re.match(r"(\S+) .*best ([\d.]+) ms  median ([\d.]+)", l)
+    if m:
+        rows[m.group(1)][0].append(float(m.group(2)))
+        rows[m.group(1)][1].append(float(m.group(3)))
+for k, (b, md) in rows.items():
+    print(k, "best", min(b), "median of bests", statistics.median(b), "median of medians", statistics.median(md), len(b))
+PY
+      ;;
     e2erows)
       : > $OUT/e2e_rows.txt
       for r in 1 2 3; do
