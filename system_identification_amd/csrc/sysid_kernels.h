@@ -400,6 +400,9 @@ __device__ __forceinline__ void panel_store_f32(__bf16* p, float a, float b) {
   v[1] = (__bf16)b;
   *reinterpret_cast<bf16x2_t*>(p) = v;
 }
+// one column (the odd column of a lane's inertia triple in the f64 / f32 Q-form)
+__device__ __forceinline__ void panel_store1(double* p, double a) { *p = a; }
+__device__ __forceinline__ void panel_store1(float* p, double a) { *p = (float)a; }
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // v of the partner lane (lane ^ 1), f32
 __device__ __forceinline__ float pair_swap_f32(float v) {
@@ -1731,140 +1734,172 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             for (int c = 0; c < 3; ++c) Kq[j][c] += qv * a3[c];
           }
         }
-        // F6[c] . [own G | partner's G] = output c of this lane's half
-        const double* bi = body + BODY_STRIDE * i;
-        double F6[6][6];
-        {
-          double FA[24], FB[18];
-          if (h == 0) body_block_mass(bi, FA);
-          else body_block_inertia(bi, FB);
+        if constexpr (std::is_same_v<OutT, __bf16>) {
+          // bf16 chunk panels (the Gram-only bf16 Gram, config 5): a 6 x 6 form in packed f32.  F6[c] . [own G |
+          // partner's G] = output c of this lane's half (an h = 1 lane's mass slots and the h = 0 lane's inertia
+          // slots are zeros: in packed f32 two columns cost one instruction, and the even split of the f64 / f32 form
+          // below measured more instructions per row here, 75 vs 69, and K1 +1.7%)
+          const double* bi = body + BODY_STRIDE * i;
+          double F6[6][6];
+          {
+            double FA[24], FB[18];
+            if (h == 0) body_block_mass(bi, FA);
+            else body_block_inertia(bi, FB);
 #pragma unroll
-          for (int c = 0; c < 6; ++c)
+            for (int c = 0; c < 6; ++c)
 #pragma unroll
-            for (int q = 0; q < 6; ++q) {
-              const int qb = (q + 3) % 6;  // the G component in slot q of an h = 1 lane (compile-time indices)
-              F6[c][q] = h == 0 ? (c < 4 ? FA[6 * c + q] : 0.0) : (qb < 3 ? 0.0 : FB[3 * c + qb - 3]);
-            }
-        }
-        OutT* oi = out + 10 * (i - 1) + 4 * h;
-        const double* jrs = Jws + c3;
-        // The row loops read row r + 1's Q entries and motion-axis components while row r is multiplied (one LDS
-        // wait per row, behind a row of arithmetic, instead of two waits up front), and store through the same
-        // three instructions in both lanes of a pair (an h = 0 lane rewrites its columns 2, 3 with the third
-        // store: no exec-masked branch per row).
-        auto rows = [&](auto kqc) {
-          constexpr int KQ = decltype(kqc)::value;
-          constexpr int KQ2 = (KQ + 1) / 2;
-          double qn[2 * KQ2], jn[3];
-          auto row_ld = [&](int r, double* qv, double* jv) {
-            const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
-#pragma unroll
-            for (int j = 0; j < KQ2; ++j) {
-              const double2 v = q2[j];
-              qv[2 * j] = v.x;
-              qv[2 * j + 1] = v.y;
-            }
-            const double* jr = jrs + 6 * r;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) jv[c] = jr[c];
-          };
-          row_ld(0, qn, jn);
-#pragma unroll 1
-          for (int r = 0; r < nrows; ++r) {
-            const double sf = ((smask >> r) & 1ull) ? 1.0 : 0.0;
-            double qr[2 * KQ2], jr[3];
-#pragma unroll
-            for (int j = 0; j < 2 * KQ2; ++j) qr[j] = qn[j];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) jr[c] = jn[c];
-            row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
-            double G[6];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) G[c] = sf * jr[c];
-#pragma unroll
-            for (int j = 0; j < KQ; ++j)
-#pragma unroll
-              for (int c = 0; c < 3; ++c) G[c] -= qr[j] * Kq[j][c];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) G[3 + c] = pair_swap(G[c]);
-            double y[6];
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-              y[c] = G[0] * F6[c][0] + G[1] * F6[c][1] + G[2] * F6[c][2] + G[3] * F6[c][3] + G[4] * F6[c][4] +
-                     G[5] * F6[c][5];
-            // outputs 4, 5 are stored by h = 1 lanes only, whose slots 3..5 (the partner's components) are zero
-#pragma unroll
-            for (int c = 4; c < 6; ++c) y[c] = G[0] * F6[c][0] + G[1] * F6[c][1] + G[2] * F6[c][2];
-            OutT* o2 = oi + (int64_t)r * ldp;
-            panel_store(o2, y[0], y[1]);
-            panel_store(o2 + 2, y[2], y[3]);
-            panel_store(o2 + (h ? 4 : 2), h ? y[4] : y[2], h ? y[5] : y[3]);
+              for (int q = 0; q < 6; ++q) {
+                const int qb = (q + 3) % 6;  // the G component in slot q of an h = 1 lane (compile-time indices)
+                F6[c][q] = h == 0 ? (c < 4 ? FA[6 * c + q] : 0.0) : (qb < 3 ? 0.0 : FB[3 * c + qb - 3]);
+              }
           }
-        };
-        // bf16 chunk panels (the Gram-only bf16 Gram, config 5): the same row loop in f32 with packed FMAs
-        // (v_pk_fma_f32: two FMAs per instruction at the cost of one f64 FMA).  G and the block's outputs carry
-        // ~1e-7 relative error, far below the bf16 rounding (2^-9) the panel gets anyway; K and F6 are formed in
-        // f64 and rounded once.
-        const float* q32 = reinterpret_cast<const float*>(wr + L.q32);  // [r][Q 0..7 | J 0..5]
-        auto rows_f32 = [&](auto kqc) {
-          constexpr int KQ = decltype(kqc)::value;
-          f32x2_t K01[KQ];
-          float K2[KQ];
-#pragma unroll
-          for (int j = 0; j < KQ; ++j) {
-            K01[j] = f32x2_t{(float)Kq[j][0], (float)Kq[j][1]};
-            K2[j] = (float)Kq[j][2];
-          }
-          f32x2_t Fp[3][6];  // Fp[p][q] = (F6[2p][q], F6[2p + 1][q])
-#pragma unroll
-          for (int pp = 0; pp < 3; ++pp)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) Fp[pp][q] = f32x2_t{(float)F6[2 * pp][q], (float)F6[2 * pp + 1][q]};
-          float qn[K1_QF_KMAX], jn[3];
-          auto row_ld = [&](int r, float* qv, float* jv) {
-            const float* qrow = q32 + 14 * r;
-#pragma unroll
-            for (int j = 0; j < K1_QF_KMAX; ++j) qv[j] = qrow[j];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) jv[c] = qrow[8 + c3 + c];
-          };
-          row_ld(0, qn, jn);
-#pragma unroll 1
-          for (int r = 0; r < nrows; ++r) {
-            const float sf = ((smask >> r) & 1ull) ? 1.0f : 0.0f;
-            float qr[K1_QF_KMAX], jr[3];
-#pragma unroll
-            for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = qn[j];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) jr[c] = jn[c];
-            row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
-            f32x2_t g01 = f32x2_t{sf * jr[0], sf * jr[1]};
-            float g2 = sf * jr[2];
+          OutT* oi = out + 10 * (i - 1) + 4 * h;
+          // The row loop reads row r + 1's Q entries and motion-axis components while row r is multiplied, and
+          // stores through the same three instructions in both lanes of a pair (an h = 0 lane rewrites its columns
+          // 2, 3 with the third store: no exec-masked branch per row).  Packed FMAs (v_pk_fma_f32: two FMAs per
+          // instruction at the cost of one f64 FMA); G and the block's outputs carry
+          // ~1e-7 relative error, far below the bf16 rounding (2^-9) the panel gets anyway; K and F6 are formed in
+          // f64 and rounded once.
+          const float* q32 = reinterpret_cast<const float*>(wr + L.q32);  // [r][Q 0..7 | J 0..5]
+          auto rows_f32 = [&](auto kqc) {
+            constexpr int KQ = decltype(kqc)::value;
+            f32x2_t K01[KQ];
+            float K2[KQ];
 #pragma unroll
             for (int j = 0; j < KQ; ++j) {
-              g01 -= qr[j] * K01[j];
-              g2 -= qr[j] * K2[j];
+              K01[j] = f32x2_t{(float)Kq[j][0], (float)Kq[j][1]};
+              K2[j] = (float)Kq[j][2];
             }
-            const float G[6] = {g01.x, g01.y, g2, pair_swap_f32(g01.x), pair_swap_f32(g01.y), pair_swap_f32(g2)};
-            f32x2_t y01 = f32x2_t{0.0f, 0.0f}, y23 = y01, y45 = y01;
+            f32x2_t Fp[3][6];  // Fp[p][q] = (F6[2p][q], F6[2p + 1][q])
 #pragma unroll
-            for (int q = 0; q < 6; ++q) {
-              y01 += G[q] * Fp[0][q];
-              y23 += G[q] * Fp[1][q];
+            for (int pp = 0; pp < 3; ++pp)
+#pragma unroll
+              for (int q = 0; q < 6; ++q) Fp[pp][q] = f32x2_t{(float)F6[2 * pp][q], (float)F6[2 * pp + 1][q]};
+            float qn[K1_QF_KMAX], jn[3];
+            auto row_ld = [&](int r, float* qv, float* jv) {
+              const float* qrow = q32 + 14 * r;
+#pragma unroll
+              for (int j = 0; j < K1_QF_KMAX; ++j) qv[j] = qrow[j];
+#pragma unroll
+              for (int c = 0; c < 3; ++c) jv[c] = qrow[8 + c3 + c];
+            };
+            row_ld(0, qn, jn);
+#pragma unroll 1
+            for (int r = 0; r < nrows; ++r) {
+              const float sf = ((smask >> r) & 1ull) ? 1.0f : 0.0f;
+              float qr[K1_QF_KMAX], jr[3];
+#pragma unroll
+              for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = qn[j];
+#pragma unroll
+              for (int c = 0; c < 3; ++c) jr[c] = jn[c];
+              row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
+              f32x2_t g01 = f32x2_t{sf * jr[0], sf * jr[1]};
+              float g2 = sf * jr[2];
+#pragma unroll
+              for (int j = 0; j < KQ; ++j) {
+                g01 -= qr[j] * K01[j];
+                g2 -= qr[j] * K2[j];
+              }
+              const float G[6] = {g01.x, g01.y, g2, pair_swap_f32(g01.x), pair_swap_f32(g01.y), pair_swap_f32(g2)};
+              f32x2_t y01 = f32x2_t{0.0f, 0.0f}, y23 = y01, y45 = y01;
+#pragma unroll
+              for (int q = 0; q < 6; ++q) {
+                y01 += G[q] * Fp[0][q];
+                y23 += G[q] * Fp[1][q];
+              }
+              // outputs 4, 5: h = 1 lanes only, whose slots 3..5 are zero
+#pragma unroll
+              for (int q = 0; q < 3; ++q) y45 += G[q] * Fp[2][q];
+              __bf16* o2 = reinterpret_cast<__bf16*>(oi + (int64_t)r * ldp);
+              panel_store_f32(o2, y01.x, y01.y);
+              panel_store_f32(o2 + 2, y23.x, y23.y);
+              panel_store_f32(o2 + (h ? 4 : 2), h ? y45.x : y23.x, h ? y45.y : y23.y);
             }
-            // outputs 4, 5: h = 1 lanes only, whose slots 3..5 are zero
-#pragma unroll
-            for (int q = 0; q < 3; ++q) y45 += G[q] * Fp[2][q];
-            __bf16* o2 = reinterpret_cast<__bf16*>(oi + (int64_t)r * ldp);
-            panel_store_f32(o2, y01.x, y01.y);
-            panel_store_f32(o2 + 2, y23.x, y23.y);
-            panel_store_f32(o2 + (h ? 4 : 2), h ? y45.x : y23.x, h ? y45.y : y23.y);
-          }
-        };
-        if constexpr (std::is_same_v<OutT, __bf16>) {
+          };
           if (kq <= 3) rows_f32(std::integral_constant<int, 3>{});
           else rows_f32(std::integral_constant<int, K1_QF_KMAX>{});
         } else {
+          // The block's ten columns split evenly between the pair: lane h takes two first-moment / mass columns (2h,
+          // 2h + 1: six-term dot products with [own | partner's] G) and three inertia columns (h = 0: 6, 7 and 4;
+          // h = 1: 8, 9 and 5: three-term products with G's angular half, which is the partner's half for h = 0 and
+          // its own for h = 1), 21 FMAs per row and lane where the 6 x 6 form took 30 (an h = 1 lane's mass slots and
+          // the h = 0 lane's inertia slots were zeros).  Both lanes store with the same instructions: the pair at 2h,
+          // the single column at 4 + h and the inertia pair at 6 + 2h.
+          const double* bi = body + BODY_STRIDE * i;
+          double F6a[2][6], F3[3][3];
+          {  // one block at a time (both live at once push the kernel over the register limit)
+            double FA[24];
+            body_block_mass(bi, FA);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+              for (int q = 0; q < 6; ++q)  // slot q: G component q (h = 0) or (q + 3) % 6 (h = 1): compile-time indices
+                F6a[a][q] = h ? FA[6 * (2 + a) + (q + 3) % 6] : FA[6 * a + q];
+          }
+          {
+            double FB[18];
+            body_block_inertia(bi, FB);
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) F3[a][j] = h ? FB[3 * (a == 2 ? 1 : 4 + a) + j] : FB[3 * (a == 2 ? 0 : 2 + a) + j];
+          }
+          OutT* oi = out + 10 * (i - 1);
+          const int o6 = 2 * h, o3 = 6 + 2 * h, o1 = 4 + h;  // column offsets of the lane's stores
+          const double* jrs = Jws + c3;
+          // The row loops read row r + 1's Q entries and motion-axis components while row r is multiplied (one LDS
+          // wait per row, behind a row of arithmetic, instead of two waits up front).
+          auto rows = [&](auto kqc) {
+            constexpr int KQ = decltype(kqc)::value;
+            constexpr int KQ2 = (KQ + 1) / 2;
+            double qn[2 * KQ2], jn[3];
+            auto row_ld = [&](int r, double* qv, double* jv) {
+              const double2* q2 = reinterpret_cast<const double2*>(Qt + r * K1_QF_KMAX);
+#pragma unroll
+              for (int j = 0; j < KQ2; ++j) {
+                const double2 v = q2[j];
+                qv[2 * j] = v.x;
+                qv[2 * j + 1] = v.y;
+              }
+              const double* jr = jrs + 6 * r;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) jv[c] = jr[c];
+            };
+            row_ld(0, qn, jn);
+#pragma unroll 1
+            for (int r = 0; r < nrows; ++r) {
+              const double sf = ((smask >> r) & 1ull) ? 1.0 : 0.0;
+              double qr[2 * KQ2], jr[3];
+#pragma unroll
+              for (int j = 0; j < 2 * KQ2; ++j) qr[j] = qn[j];
+#pragma unroll
+              for (int c = 0; c < 3; ++c) jr[c] = jn[c];
+              row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
+              double G[6];
+#pragma unroll
+              for (int c = 0; c < 3; ++c) G[c] = sf * jr[c];
+#pragma unroll
+              for (int j = 0; j < KQ; ++j)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) G[c] -= qr[j] * Kq[j][c];
+#pragma unroll
+              for (int c = 0; c < 3; ++c) G[3 + c] = pair_swap(G[c]);
+              double ga[3];  // G's angular half
+#pragma unroll
+              for (int c = 0; c < 3; ++c) ga[c] = h ? G[c] : G[3 + c];
+              double y6[2], y3[3];
+#pragma unroll
+              for (int a = 0; a < 2; ++a)
+                y6[a] = G[0] * F6a[a][0] + G[1] * F6a[a][1] + G[2] * F6a[a][2] + G[3] * F6a[a][3] +
+                        G[4] * F6a[a][4] + G[5] * F6a[a][5];
+#pragma unroll
+              for (int a = 0; a < 3; ++a) y3[a] = ga[0] * F3[a][0] + ga[1] * F3[a][1] + ga[2] * F3[a][2];
+              OutT* o2 = oi + (int64_t)r * ldp;
+              panel_store(o2 + o6, y6[0], y6[1]);
+              panel_store(o2 + o3, y3[0], y3[1]);
+              panel_store1(o2 + o1, y3[2]);
+            }
+          };
           if (kq <= 3) rows(std::integral_constant<int, 3>{});
           else rows(std::integral_constant<int, K1_QF_KMAX>{});
         }
