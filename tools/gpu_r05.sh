@@ -23,7 +23,7 @@ for step in "$@"; do
       python tools/bench_summary.py $OUT/bench_spot_gram_only.json ;;
     stamps)
       SYSID_LIB=$PWD/tools/_libs/stamps0.so timeout -k 10 200 python tools/ab/k1_stamps_run.py spot 20000 f64 > $OUT/stamps_spot.txt 2>&1 || { echo "stamps failed"; tail $OUT/stamps_spot.txt; exit 1; }
-      SYSID_LIB=$PWD/tools/_libs/stamps2.so timeout -k 10 200 python tools/ab/k1_stamps_run.py g1_29dof 125000 bf16 > $OUT/stamps_g1_bf16.txt 2>&1 || { echo "stamps g1 failed"; tail $OUT/stamps_g1_bf16.txt; exit 1; }
+      SYSID_LIB=$PWD/tools/_libs/stamps0.so timeout -k 10 200 python tools/ab/k1_stamps_run.py g1_29dof 125000 bf16 > $OUT/stamps_g1_bf16.txt 2>&1 || { echo "stamps g1 failed"; tail $OUT/stamps_g1_bf16.txt; exit 1; }
       cat $OUT/stamps_spot.txt $OUT/stamps_g1_bf16.txt | grep -v amdgpu.ids ;;
     g1bf16)
       timeout -k 10 300 python bench.py --robot g1_29dof --samples 125000 --gram-only --precision bf16 --no-cpu-baseline --no-e2e --steps 10 --warmup 3 > $OUT/bench_g1_125k_bf16.json 2> $OUT/bench_g1.err || { echo "g1 bench failed"; tail -20 $OUT/bench_g1.err; exit 1; }
