@@ -395,18 +395,7 @@ def main():
     # re-timing, before the host-entry-point legs (whose host-bound gaps let the clocks drop again), so it sees the
     # kernels at the clocks rocprofv3's average over the same run sees them.
     n_time = N
-    fused = eng.fused(tflags & ~0x7 if args.gram_only else flags)  # K12: K1 + Gram in one launch (ms[1] = 0)
     ms = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-    ms_unfused, ms_fused = None, None
-    if fused:  # the same stages with fusion off, for the record (K1 -> K2 -> K3 as three launches)
-        eng.set_fusion(False)
-        ms_unfused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-        eng.set_fusion(True)
-    else:  # fusion off (the default: measured slower), the fused kernel's time for the record where it exists
-        eng.set_fusion(True)
-        if eng.fused(tflags & ~0x7 if args.gram_only else flags):
-            ms_fused = eng.time_stages(d_in, N, tflags if args.gram_only else flags, bufs, iters=max(5, args.steps))
-        eng.set_fusion(False)
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = e2e_legs(eng, data, N)
@@ -427,23 +416,7 @@ def main():
         # nv-row count stays in K2_TFps / gram_gflops
         rows_per_sample = float(np.mean(nv - 3 * (data["contact"] != 0).sum(axis=0)))
     k2_exec_tfs = k2_tfs * rows_per_sample / nv
-    if fused:
-        # the fused kernel does K1's HBM work and the Gram's MFMA work in one launch; the MFMA side is its floor
-        # (Spot 20k: 8.70 GFLOP at 78.6 TF/s = 0.111 ms against 458 MB of HBM writes at 8 TB/s = 0.057 ms)
-        traffic, src = pmc_traffic("k12_fused_panel_gram", args.robot, N)
-        peak = MFMA_PEAK_TFS["f64"]
-        k12_tfs = n_time * flops_k2 / (ms[0] * 1e-3) / 1e12
-        hbm_b = n_time * (in_b + (0 if args.gram_only else panel_b))
-        roof = {"kernel": "k12_fused_panel_gram", "bound": "mfma", "achieved": round(k12_tfs, 3), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(k12_tfs / peak, 4), "traffic": traffic, "traffic_source": src,
-                "algorithmic_flops_per_launch": round(n_time * flops_k2),
-                "algorithmic_hbm_bytes_per_launch": hbm_b,
-                "hbm_achieved_GBps": round(hbm_b / (ms[0] * 1e-3) / 1e9, 1),
-                "avg_launch_ms": round(ms[0], 5),
-                "note": "K1 (regressor + projector rows) and K2 (Gram MFMA) in one launch, the rows re-read from "
-                        "L2, not HBM" + ("; Gram-only: the rows never reach HBM (per-wave rings)" if args.gram_only
-                                         else "")}
-    elif ms[0] >= ms[1]:
+    if ms[0] >= ms[1]:
         traffic, src = pmc_traffic("k1_regressor_panel", args.robot, N) if not args.gram_only else (None, None)
         roof = {"kernel": "k1_regressor_panel", "bound": "hbm", "achieved": round(k1_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
@@ -468,7 +441,7 @@ def main():
                   "source": "HIP events on the launch stream between consecutive timed steps (rank 0)"}
     # step-level floor: the bytes the step must move (inputs + panel written by K1 and read back by K2; Gram-only
     # chunks may stay on-die and are not counted) at HBM peak, and the Gram flops at the MFMA peak
-    step_bytes = N * (in_b + (0 if args.gram_only else (1 if fused else 2) * panel_b))
+    step_bytes = N * (in_b + (0 if args.gram_only else 2 * panel_b))
     hbm_floor = step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
     mfma_floor = N * flops_k2 / (MFMA_PEAK_TFS[args.precision if args.gram_only else "f64"] * 1e12) * 1e3
     value = total_per_step * args.steps / elapsed
@@ -482,33 +455,23 @@ def main():
                 "inverse-dynamics torques + noise, trot contacts with LOST=2); no .dat ships with the reference",
         "config": {"workload": f"{args.robot} " + (f"{args.total_samples} samples split over {world} GPU(s)" if strong
                                                     else f"{N} samples per GPU") + ", " + (
-                       (f"Gram only ({rows_used} rows through the fused kernel's on-die rings, {args.precision} Gram)"
-                        if fused else f"Gram only ({rows_used} rows chunked on the device, {args.precision} Gram)")
+                       f"Gram only ({rows_used} rows chunked on the device, {args.precision} Gram)"
                        if args.gram_only else
                        "full outputs (stacked Y_proj/tau_proj/B_v/B_c panel + Gram)"),
                    "robot": args.robot, "samples_per_gpu": N, "total_samples_per_step": total_per_step,
                    "nv": nv, "W": W, "parallelism": f"dp{world}",
                    "exchange": exchange_name,
                    "exchange_check": exchange_check,
-                   "timed_region": (("fused K1 + Gram (K12) + K3" + (" (Gram-only)" if args.gram_only else "")) if fused
-                                    else "K1 + K2 per panel chunk + K3 (Gram-only)" if args.gram_only else "K1 + K2 + K3")
+                   "timed_region": ("K1 + K2 per panel chunk + K3 (Gram-only)" if args.gram_only else "K1 + K2 + K3")
                    + ", HBM-resident inputs and outputs" + (", + the Gram all-reduce" if comm is not None or world > 1
                                                              else "")},
         "step_times": step_stats,
         "settle": settle,
         "steady_state": steady,
         "gram_gflops": round(total_per_step * flops_k2 / (ms_step * 1e-3) / 1e9, 2),
-        "kernel_ms": ({"K12_fused_panel_gram": round(ms[0], 5), "K3_gram_reduce": round(ms[2], 5),
-                       "samples_timed": n_time} if fused else
-                      {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
-                       "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time}),
-        "kernel_ms_unfused": None if ms_unfused is None else {
-            "K1_regressor_panel": round(ms_unfused[0], 5), "K2_gram_syrk": round(ms_unfused[1], 5),
-            "K3_gram_reduce": round(ms_unfused[2], 5), "note": "the same step with fusion off (sysid_set_fusion)"},
-        "kernel_ms_fused": None if ms_fused is None else {
-            "K12_fused_panel_gram": round(ms_fused[0], 5), "K3_gram_reduce": round(ms_fused[2], 5),
-            "note": "the same step with the fused K1 + Gram kernel (sysid_set_fusion(1), off by default: slower)"},
-        "K1_GBps": None if fused else round(k1_gbs, 1), "K2_TFps": None if fused else round(k2_tfs, 3),
+        "kernel_ms": {"K1_regressor_panel": round(ms[0], 5), "K2_gram_syrk": round(ms[1], 5),
+                      "K3_gram_reduce": round(ms[2], 5), "samples_timed": n_time},
+        "K1_GBps": round(k1_gbs, 1), "K2_TFps": round(k2_tfs, 3),
         "roofline": roof,
         "step_roofline": {"hbm_bytes": step_bytes, "hbm_floor_ms": round(hbm_floor, 5),
                           "mfma_floor_ms": round(mfma_floor, 5), "floor_ms": round(max(hbm_floor, mfma_floor), 5),

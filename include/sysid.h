@@ -91,7 +91,7 @@ extern "C" {
 typedef struct sysid_engine sysid_engine;
 
 /* ABI version (bumped on any signature or layout change). */
-int32_t sysid_abi_version(void);  /* 7 */
+int32_t sysid_abi_version(void);  /* 8 */
 
 /* Create an engine for one device from a packed model.  Replaces the model construction of
  * SystemIdentification.__init__ (src/sys_identification.py:11-73; pin.buildModelFromUrdf at :16). */
@@ -120,7 +120,7 @@ int32_t sysid_build(sysid_engine* e, const double* q, const double* dq, const do
 /* sysid_build with q and cnt in float32, the dtypes read_data returns them in (demo/spot_identification.py:10-14:
  * np.loadtxt(..., dtype=np.float32); the Butterworth filter at :20-25 makes dq, ddq and tau float64).  Same outputs
  * and behaviour; the inputs cross PCIe as q float32 and one byte per contact value (the non-zero test is all the
- * projector reads: `if contact_scedule[index]`, src/sys_identification.py:125), 461 instead of 568 bytes per Spot
+ * projector reads: `if contact_scedule[index]`, src/sys_identification.py:125), 464 instead of 568 bytes per Spot
  * sample, and are widened exactly on the device.  Replaces the same reference interface as sysid_build. */
 int32_t sysid_build_f32qc(sysid_engine* e, const float* q, const double* dq, const double* ddq,
                           const double* tau, const float* cnt, int64_t N, int64_t ld, uint32_t flags,
@@ -166,8 +166,7 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
  * sysid_gram_workspace_bytes reports follows it.  That workspace is exactly: 1 KiB of K1 sample counters, the
  * chunk panel (min(chunk bytes, N·nv rows of the Gram's element type)), the split-K slabs (K2 workgroups x
  * Gram tile slots x 2 KiB: Spot <= 29 MB, G1 <= 141 MB) and, for the nullspace rows, 4·(nv + 1) bytes per
- * chunk sample of row counts and row list plus 4 bytes per 1024 samples of segment sums; while the fused kernel is
- * on (sysid_set_fusion, quadrupeds, f64) at least its rings (~140 MB) and slabs.  A workspace sized before a change
+ * chunk sample of row counts and row list plus 4 bytes per 1024 samples of segment sums.  A workspace sized before a change
  * of these settings is checked again at launch (SYSID_E_INVALID when short, never overrun).  Fewer, larger chunks
  * are faster (each costs a K1 launch tail and a pass over the split-K slabs: 16 GiB is 2-3% faster than 4 GiB
  * on G1 1M); a smaller chunk bounds the device memory of very large N. */
@@ -248,22 +247,6 @@ int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4);
 /* K2 Gram deal chosen at model creation: {tile columns, tile slots of the f64, f32 and bf16 deals}. */
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
 
-/* Fused K1 + Gram (k12_fused_panel_gram): the f64 paths of the quadruped models (nv = 18, a 10-tile Gram: Spot,
- * Solo-12) build the projected rows and the Gram in one launch, the Gram waves reading each pair of samples'
- * rows back from L2 while the K1 waves of their workgroup produce the next ones.  Full outputs
- * (sysid_build_device with SYSID_EMIT_GRAM and the engine's panel_ld): the stacked panel is written as before.
- * Gram-only (sysid_build_gram_device, f64, projector rows): the rows go through per-wave rings of three sample
- * pairs in the workspace (~140 MB, they stay on-die) instead of chunk panels; SYSID_GRAM_NULLSPACE keeps the
- * unfused nullspace-row path.  Same outputs and contracts (the Gram differs from the unfused path's only in
- * summation order, ~1e-16 relative).  Off by default: beside the Gram waves the K1 waves run at half their
- * standalone occupancy (both are register-bound at two waves per SIMD), so the fused launch measured slower than
- * K1 -> K2 -> K3 (Spot 20k: 0.445 vs 0.37 ms).  sysid_set_fusion (or SYSID_FUSE=1 at engine creation) turns
- * it on; sysid_fused tells whether `flags` run fused (with a stacked-output flag: sysid_build_device; without:
- * sysid_build_gram_device).  Every wait between the two roles is bounded (~1 s): a wave that gives up sets its
- * workgroup's abort word, the Gram waves then write NaN tiles and later waits return at once, so a defect shows
- * in the Gram instead of hanging the device. */
-int32_t sysid_set_fusion(sysid_engine* e, int32_t on);
-int32_t sysid_fused(const sysid_engine* e, uint32_t flags);
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */
 int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6);
 

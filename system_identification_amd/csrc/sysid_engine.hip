@@ -80,14 +80,18 @@ class HostPool {
   }
 
  private:
-  static constexpr int SPIN_US = 2000;
+  // After a job a worker polls for the next one for SPIN_US before it blocks: back-to-back host calls (~0.5 ms
+  // apart) then skip the condition-variable wake-up.  The poll pauses between reads (no clock read per iteration),
+  // so an idle engine costs at most ~1 ms of mostly paused core time per worker and call.
+  static constexpr int SPIN_US = 1000;
   void loop(int t) {
     uint64_t seen = 0;
     for (;;) {
       std::function<void(int)> f;
       const auto spin_end = std::chrono::steady_clock::now() + std::chrono::microseconds(SPIN_US);
-      while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed) &&
-             std::chrono::steady_clock::now() < spin_end) {
+      for (int it = 0; gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed); ++it) {
+        __builtin_ia32_pause();
+        if ((it & 63) == 63 && std::chrono::steady_clock::now() >= spin_end) break;
       }
       {
         std::unique_lock<std::mutex> g(m_);
@@ -142,11 +146,6 @@ struct sysid_engine {
     int blk = 0;  // the register-blocked kernel (k2_gram_syrk_blk / _bf16_blk): one workgroup per CU
     int2* d_tiles = nullptr;  // [super slots | tile slots]
   } k2d[3];
-  // K12: the fused K1 + Gram kernel of the full-output f64 path (quadruped K1, 10 tile columns): usable (k12_ok),
-  // enabled (fuse: sysid_set_fusion), its dynamic LDS and the K3 tile table of its slab slots
-  int k12_ok = 0, fuse = 0;  // the fused kernel is opt-in: measured slower
-  size_t k12_lds = 0;
-  int2* d_k12_tiles = nullptr;
   // host-API buffers (grow-only)
   double* d_in = nullptr;
   size_t in_cap = 0;
@@ -185,6 +184,23 @@ int set_err(sysid_engine* e, int code, const char* fmt, ...) {
   g_thread_error = buf;
   return code;
 }
+
+// The engine's device for the duration of one entry point, the caller's current device restored on return: a C-ABI
+// call must not change the calling thread's device (PyTorch reads it for its own allocations).
+struct DevScope {
+  int prev = -1;
+  hipError_t st = hipSuccess;
+  explicit DevScope(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) st = hipSetDevice(d);
+  }
+  ~DevScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DevScope(const DevScope&) = delete;
+  DevScope& operator=(const DevScope&) = delete;
+};
 
 #define HIP_TRY(e, expr)                                                                       \
   do {                                                                                         \
@@ -343,49 +359,12 @@ int launch_k3(sysid_engine* e, int ks, const double* slab, double* d_gram, hipSt
   return SYSID_OK;
 }
 
-// K12 (fused K1 + Gram): one workgroup per CU, at most one per sample pair.
-int64_t k12_grid(const sysid_engine* e, int64_t N) {
-  return std::max<int64_t>(1, std::min<int64_t>(e->cus, (N + 1) / 2));
-}
-size_t k12_slab_bytes(const sysid_engine* e, int64_t N) {
-  return align256((size_t)k12_grid(e, N) * K12_NSLOTS * 256 * sizeof(double));
-}
-// The full-output Gram runs fused when the model has the kernel, fusion is on, the Gram is f64 and the panel has
-// the engine's own leading dimension (the Gram waves read exactly the columns K1 writes).
-bool k12_active(const sysid_engine* e, uint32_t flags, int64_t ld_panel) {
-  return e->k12_ok && e->fuse && (flags & SYSID_EMIT_GRAM) && gram_prec(flags) == 0 && ld_panel == e->ldp;
-}
-
-int launch_k12(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel,
-               double* slab, hipStream_t st, int ring = 0) {
-  K1Params kp = e->kp;
-  const sysid_engine::K1Shape& K = e->k1m[0];
-  kp.pov = 0;
-  kp.wave_dbl = K.wave_dbl;
-  kp.rg = k1_row_groups(kp.NJ, 64 / k1_spw(K.variant));
-  kp.out_cols = (int)std::min<int64_t>(ld_panel, e->ldp);
-  sysid_launch::k12_launch(ring, dim3((unsigned)k12_grid(e, N)), e->k12_lds, st, kp, e->d_mimg, d_in, N, ld, d_panel,
-                           ld_panel, slab);
-  HIP_TRY(e, hipGetLastError());
-  return SYSID_OK;
-}
-
-int launch_k3_tiles(sysid_engine* e, int ks, const double* slab, const int2* tiles, int nslots, double* d_gram,
-                    hipStream_t st) {
-  const int64_t nx = (int64_t)nslots * 256;
-  hipLaunchKernelGGL(k3_gram_reduce, dim3((unsigned)(nx / 64)), dim3(1024), 0, st, slab, tiles, nx, ks, e->ncol,
-                     d_gram);
-  HIP_TRY(e, hipGetLastError());
-  return SYSID_OK;
-}
-
-// Workspace of sysid_build_device: [K1 counter | K2 slabs] (the slabs with EMIT_GRAM: room for the unfused K2's
-// and the fused kernel's, whichever runs).
+// Workspace of sysid_build_device: [K1 counter | K2 slabs] (the slabs with EMIT_GRAM).
 size_t stages_ws_bytes(const sysid_engine* e, int64_t N, uint32_t flags) {
   if (N <= 0) return 0;
   const int64_t rows = N * e->nv;
   size_t slabs = 0;
-  if (flags & SYSID_EMIT_GRAM) slabs = std::max(slab_bytes(e, rows), e->k12_ok ? k12_slab_bytes(e, N) : (size_t)0);
+  if (flags & SYSID_EMIT_GRAM) slabs = slab_bytes(e, rows);
   return WORK_BYTES + slabs;
 }
 
@@ -413,20 +392,6 @@ int launch_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, ui
   if (rc != SYSID_OK) return rc;
   const int64_t rows = N * e->nv;
   auto* work = static_cast<unsigned long long*>(d_ws);
-  if (k12_active(e, flags, ld_panel)) {
-    // fused: K1 + Gram in one launch (events: [0] -> [1] the fused kernel, [1] -> [2] empty, [2] -> [3] K3)
-    double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-    if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
-    if ((rc = launch_k12(e, d_in, N, ld, d_panel, ld_panel, slab, st)) != SYSID_OK) return rc;
-    if (ev) {
-      HIP_TRY(e, hipEventRecord(ev[1], st));
-      HIP_TRY(e, hipEventRecord(ev[2], st));
-    }
-    if ((rc = launch_k3_tiles(e, (int)k12_grid(e, N), slab, e->d_k12_tiles, K12_NSLOTS, d_gram, st)) != SYSID_OK)
-      return rc;
-    if (ev) HIP_TRY(e, hipEventRecord(ev[3], st));
-    return SYSID_OK;
-  }
   if (ev) HIP_TRY(e, hipEventRecord(ev[0], st));
   if ((rc = launch_k1(e, d_in, N, ld, d_panel, ld_panel, work, st, nullptr, 0, 0, 0, nullptr, zeroed)) != SYSID_OK)
     return rc;
@@ -475,23 +440,12 @@ size_t cmp_tail_bytes(const sysid_engine* e, int64_t C) {
   return align256((size_t)C * 4) + align256((size_t)C * e->nv * 4);
 }
 
-// The fused Gram-only form (k12 ring): [K1 counters | slabs | rings]; rings of K12_RING two-sample slots per K1
-// wave, one row of slack for the over-read of the last row (k12_gram_wave).
-size_t k12_ring_bytes(const sysid_engine* e, int64_t N) {
-  return align256(((size_t)k12_grid(e, N) * K1_WAVES * sysid_launch::K12_RING * 2 * e->nv + 1) * e->ldp * sizeof(double));
-}
-size_t k12_ring_ws_bytes(const sysid_engine* e, int64_t N) {
-  return WORK_BYTES + k12_slab_bytes(e, N) + k12_ring_bytes(e, N);
-}
-
 // [K1 counters | row total, segment sums | panel chunk | K2 slabs | row counts | row list]
 size_t gram_ws_bytes_prec(const sysid_engine* e, int64_t N, int prec) {
   const int64_t C = gram_chunk(e, N, prec), rows = C * e->nv;
   const size_t chunked = WORK_BYTES + cmp_head_bytes(C) + align256((size_t)rows * gram_ld(e, prec) * prec_bytes(prec)) +
                          slab_bytes(e, rows, prec) + cmp_tail_bytes(e, C);
-  // the fused ring form's rings only while fusion is on (sysid_set_fusion): a workspace sized before the fusion is
-  // switched on is refused at launch (gram_ws_bytes_prec is checked there), never overrun
-  return prec == 0 && e->k12_ok && e->fuse ? std::max(chunked, k12_ring_ws_bytes(e, N)) : chunked;
+  return chunked;
 }
 
 size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every precision
@@ -507,8 +461,6 @@ size_t gram_ws_bytes(const sysid_engine* e, int64_t N) {  // enough for every pr
 // 31 of 35 rows anyway) or are bf16 (narrow Grams: the gathered rows cost the bf16 K2 more than they save).
 int gram_nullspace(const sysid_engine* e, uint32_t flags) {
   const int prec = gram_prec(flags);
-  // the fused Gram-only kernel (f64, quadrupeds) streams the projector rows through its rings
-  if (prec == 0 && e->k12_ok && e->fuse && !(flags & SYSID_GRAM_NULLSPACE)) return 0;
   const bool want_ns = (flags & SYSID_GRAM_NULLSPACE)   ? true
                        : (flags & SYSID_GRAM_PROJECTOR) ? false
                                                         : prec != 2 && !e->k1m[prec].qf;
@@ -519,11 +471,6 @@ int gram_nullspace(const sysid_engine* e, uint32_t flags) {
 int64_t k1_round_samples(const sysid_engine* e, int prec, int cmp) {
   const sysid_engine::K1Shape& K = cmp ? e->k1c[prec] : e->k1m[prec];
   return (int64_t)e->cus * K.bpc * K.waves * k1_spw(K.variant);
-}
-
-// the Gram-only path runs the fused K1 + Gram kernel (K12): f64 projector rows on a model with a K12 form, fusion on
-bool gram_fused(const sysid_engine* e, uint32_t flags) {
-  return gram_prec(flags) == 0 && !gram_nullspace(e, flags) && e->k12_ok && e->fuse;
 }
 
 // staged (host entry point): the staged chunks' bounds (staged chunk k = samples [b[k], b[k+1])), and
@@ -541,25 +488,6 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
     return set_err(e, SYSID_E_INVALID, "workspace too small: %zu < %zu bytes", d_ws ? ws_bytes : 0,
                    gram_ws_bytes_prec(e, N, prec));
   if (reinterpret_cast<uintptr_t>(d_ws) & 255) return set_err(e, SYSID_E_INVALID, "workspace must be 256-byte aligned");
-  if (gram_fused(e, flags)) {
-    // fused: K1 + Gram over all N in one launch, the rows through per-wave rings that stay on-die; events as the
-    // chunked form's (chunk 0's "K1" = the fused kernel, every other stage 0, then K3)
-    double* slab = reinterpret_cast<double*>(static_cast<char*>(d_ws) + WORK_BYTES);
-    double* ring = reinterpret_cast<double*>(reinterpret_cast<char*>(slab) + k12_slab_bytes(e, N));
-    size_t k = 0;
-    auto mark = [&]() -> int {
-      if (ev && k < ev->size()) HIP_TRY(e, hipEventRecord((*ev)[k++], st));
-      return SYSID_OK;
-    };
-    int rc;
-    if (stage_upto && (rc = (*stage_upto)(N)) < 0) return rc;  // every chunk's DMA
-    if ((rc = mark())) return rc;
-    if ((rc = launch_k12(e, d_in, N, ld, ring, e->ldp, slab, st, 1))) return rc;
-    while (ev && k + 1 < ev->size())
-      if ((rc = mark())) return rc;
-    if ((rc = launch_k3_tiles(e, (int)k12_grid(e, N), slab, e->d_k12_tiles, K12_NSLOTS, d_gram, st))) return rc;
-    return mark();
-  }
   const int64_t C = gram_chunk(e, N, prec), rows0 = C * e->nv, ldc = gram_ld(e, prec);
   if (rows0 >= ((int64_t)1 << 31)) return set_err(e, SYSID_E_INVALID, "Gram-only chunk of %lld rows", (long long)rows0);
   auto* work = static_cast<unsigned long long*>(d_ws);
@@ -695,7 +623,7 @@ hipStream_t copy_stream_of(const sysid_engine* e, int c) {
 // Wire format of the host entry points' inputs (K0W, sysid_kernels.h): per staged chunk of n samples, the q rows in
 // the caller's element type (float32 from read_data, demo/spot_identification.py:10, or float64), the dq / ddq / tau
 // rows in float64 and the contact rows as one byte each (non-zero flag); sections 16-byte aligned.  Spot with float32
-// q: 461 instead of 568 bytes per sample over PCIe.
+// q: 464 instead of 568 bytes per sample over PCIe (19·4 + 48·8 + 4).
 struct Wire {
   int64_t d, c, bytes;  // byte offsets of the float64 rows and of the contact bytes; block size
 };
@@ -912,7 +840,7 @@ int launch_k5(sysid_engine* e, const double* d_panel, int64_t rows, int64_t ld_p
 
 extern "C" {
 
-int32_t sysid_abi_version(void) { return 7; }
+int32_t sysid_abi_version(void) { return 8; }
 
 const char* sysid_last_error(const sysid_engine* e) { return e ? e->err.c_str() : g_thread_error.c_str(); }
 
@@ -1058,11 +986,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   kp.thr_rel = 1e-14;  // rank cut of the Gram-Schmidt projector (pinv: 1e-15 sigma_max)
   kp.thr_rel2 = kp.thr_rel * kp.thr_rel;
   kp.g0 = g[0]; kp.g1 = g[1]; kp.g2 = g[2];
-  kp.k12_spin_log2 = 23;   // the fused kernel's wait bound (~1 s)
-  kp.k12_stall_polls = 0;
-  // tests only: a short wait bound and held-back Gram waves exercise the fused kernel's give-up path
-  if (const char* v = std::getenv("SYSID_K12_SPIN_LOG2")) kp.k12_spin_log2 = std::max(1, std::min(23, std::atoi(v)));
-  if (const char* v = std::getenv("SYSID_K12_STALL_POLLS")) kp.k12_stall_polls = std::max(0, std::atoi(v));
   e->k1_maxch_tpl = maxch_tpl;
 
   // Gram tiling: 16x16 tiles grouped in 2x2 super-tiles (upper triangle of the super grid);
@@ -1205,7 +1128,8 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
     }
   }
 
-  hipError_t st = hipSetDevice(device);
+  DevScope dev_scope(device);
+  hipError_t st = dev_scope.st;
   hipDeviceProp_t prop;
   if (st == hipSuccess) st = hipGetDeviceProperties(&prop, device);
   if (st == hipSuccess) e->cus = prop.multiProcessorCount;
@@ -1270,28 +1194,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       sysid_destroy(e);
       return SYSID_E_MODEL;
     }
-    // the fused K1 + Gram kernel: the quadruped K1 beside the 10-column Gram waves, one workgroup per CU
-    if (e->k1m[0].variant == K1_C4_NV18 && e->ntc == K12_NTC) {
-      const size_t lds = (size_t)(MI.ndbl + K1_WAVES * k1_spw(K1_C4_NV18) * e->k1m[0].wave_dbl) * sizeof(double) +
-                         (2 * K1_WAVES + 2) * sizeof(int);  // + the ready / consumed counters, the abort word
-      int nb = 0;
-      if (lds <= 160 * 1024 &&
-          hipFuncSetAttribute(sysid_launch::k12_fn(0), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
-          hipFuncSetAttribute(sysid_launch::k12_fn(1), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess &&
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sysid_launch::k12_fn(0), 64 * (K1_WAVES + K12_GW), lds) ==
-              hipSuccess &&
-          nb >= 1) {
-        std::vector<int2> tl(K12_NSLOTS);
-        for (int k = 0; k < K12_NSLOTS; ++k) tl[k] = k12_tile(k);
-        st = hipMalloc(&e->d_k12_tiles, tl.size() * sizeof(int2));
-        if (st == hipSuccess) st = hipMemcpy(e->d_k12_tiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice);
-        e->k12_ok = st == hipSuccess ? 1 : 0;
-        e->k12_lds = lds;
-        if (const char* v = std::getenv("SYSID_FUSE")) e->fuse = std::atoi(v) != 0 ? 1 : 0;
-      } else {
-        (void)hipGetLastError();
-      }
-    }
   }
   if (st != hipSuccess) {
     set_err(nullptr, SYSID_E_DEVICE, "device setup failed: %s", hipGetErrorString(st));
@@ -1304,9 +1206,9 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
 
 void sysid_destroy(sysid_engine* e) {
   if (!e) return;
-  (void)hipSetDevice(e->device);
+  DevScope dev_scope(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_k12_tiles, (void*)e->d_in, (void*)e->d_panel,
+  for (void* p : {(void*)e->d_mimg, (void*)e->d_work, (void*)e->k2d[0].d_tiles, (void*)e->k2d[1].d_tiles, (void*)e->k2d[2].d_tiles, (void*)e->d_in, (void*)e->d_panel,
                   (void*)e->d_gram, e->d_ws, (void*)e->d_out, (void*)e->d_dump})
     if (p) (void)hipFree(p);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -1351,7 +1253,8 @@ int32_t sysid_build_device(sysid_engine* e, const double* d_in, int64_t N, int64
   if ((flags & SYSID_EMIT_GRAM) && !d_gram) return set_err(e, SYSID_E_INVALID, "EMIT_GRAM without gram buffer");
   if (reinterpret_cast<uintptr_t>(d_panel) & 15)
     return set_err(e, SYSID_E_INVALID, "d_panel must be 16-byte aligned (the panel is written with 16-byte stores)");
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     if (flags & SYSID_EMIT_GRAM)
@@ -1371,7 +1274,8 @@ int32_t sysid_build_gram_device(sysid_engine* e, const double* d_in, int64_t N, 
   if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
   if (N < 0 || ld < N || (N > 0 && !d_in) || !d_gram)
     return set_err(e, SYSID_E_INVALID, "bad arguments (N=%lld ld=%lld)", (long long)N, (long long)ld);
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     HIP_TRY(e, zero_async(d_gram, (size_t)e->ncol * e->ncol * sizeof(double), st));
@@ -1391,7 +1295,8 @@ int32_t sysid_tau_error_device(sysid_engine* e, const double* d_panel, int64_t l
   if (N < 0 || ld_panel < e->ncol || (ld_panel & 1) || !d_phi || !d_err_sq || (N > 0 && !d_panel) ||
       (reinterpret_cast<uintptr_t>(d_panel) & 15))
     return set_err(e, SYSID_E_INVALID, "bad arguments");
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   hipStream_t st = static_cast<hipStream_t>(stream);  // NULL: the null stream (see sysid.h)
   if (N == 0) {
     HIP_TRY(e, zero_async(d_err_sq, (size_t)e->nv * sizeof(double), st));
@@ -1414,7 +1319,8 @@ int32_t sysid_tau_error(sysid_engine* e, const double* q, const double* dq, cons
     const int rc = sysid_check_contacts(e, cnt, N, ld, nullptr);
     if (rc != SYSID_OK) return rc;
   }
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   const int64_t rows = N * e->nv;
   int rc;
   if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double)))) return rc;
@@ -1465,7 +1371,8 @@ int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, con
       return set_err(e, SYSID_E_CONTACT, "sample %lld: int(sum(contact)) = %g != %lld feet in contact (J_c^T lambda "
                      "has mismatched shapes in the reference)", (long long)s, std::trunc(sum), (long long)nz);
   }
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   const int64_t rows = N * e->nv;
   int rc;
   if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_lds * N * sizeof(double)))) return rc;
@@ -1505,7 +1412,8 @@ int32_t sysid_build_full(sysid_engine* e, const double* q, const double* dq, con
 int32_t sysid_time_stages(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, uint32_t flags, double* d_panel,
                           int64_t ld_panel, double* d_gram, void* d_ws, size_t ws_bytes, int32_t iters, double* ms) {
   if (!e || !ms || iters <= 0 || N <= 0) return set_err(e, SYSID_E_INVALID, "bad arguments");
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   HIP_TRY(e, hipDeviceSynchronize());  // the caller's buffers, written on any stream, are complete
   double acc[3] = {0, 0, 0};
   int rc = SYSID_OK;
@@ -1600,7 +1508,8 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
   const bool want_gram = (flags & SYSID_EMIT_GRAM) && (gram || Atb || btb);
   if (want_gram) flags |= SYSID_EMIT_GRAM; else flags &= ~SYSID_EMIT_GRAM;
   tph[0] = ms_since(t0);  // contact check
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   if (N == 0) {
     const size_t W = (size_t)e->w;
     if (gram) std::memset(gram, 0, W * W * sizeof(double));
@@ -1822,7 +1731,8 @@ int32_t sysid_debug_lds(sysid_engine* e, const double* q, const double* dq, cons
   if (!e || !lds_image) return set_err(e, SYSID_E_INVALID, "null argument");
   const WLay L = wave_layout(e->in_lds, e->nv, e->nb + 1, e->nc, k1_layout_hw(e->k1m[0].variant), e->k1m[0].pov, e->k1m[0].qf);
   if (image_doubles < L.total) return set_err(e, SYSID_E_INVALID, "image needs %d doubles", L.total);
-  HIP_TRY(e, hipSetDevice(e->device));
+  DevScope dev_scope(e->device);
+  HIP_TRY(e, dev_scope.st);
   int rc = sysid_build(e, q, dq, ddq, tau, cnt, 1, 1, SYSID_EMIT_Y, nullptr, nullptr, nullptr, nullptr, nullptr,
                        nullptr, nullptr);  // allocates the device buffers
   if (rc != SYSID_OK) return rc;
@@ -1887,30 +1797,21 @@ size_t sysid_exchange_bytes(const sysid_engine* e) {
 // sysid_rccl.cpp's hooks (one library, so the RCCL translation unit stays free of device code)
 int32_t sysid_internal_xchg_pack(const sysid_engine* e, const double* d_gram, double rows, double* d_x, void* stream) {
   const int n = e->ncol;
-  // a NULL stream is the null stream of the CURRENT device: make that the engine's (the unpack follows on it)
-  if (hipSetDevice(e->device) != hipSuccess) return SYSID_E_DEVICE;
+  // a NULL stream is the null stream of the CURRENT device: the engine's for this call (the caller's device is
+  // restored on return, DevScope)
+  DevScope dev_scope(e->device);
+  if (dev_scope.st != hipSuccess) return SYSID_E_DEVICE;
   hipLaunchKernelGGL(xchg_pack, dim3((unsigned)(((int64_t)n * n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), d_gram, n, rows, d_x);
   return hipGetLastError() == hipSuccess ? SYSID_OK : SYSID_E_DEVICE;
 }
 int32_t sysid_internal_xchg_unpack(const sysid_engine* e, const double* d_x, double* d_gram, void* stream) {
   const int n = e->ncol;
+  DevScope dev_scope(e->device);
+  if (dev_scope.st != hipSuccess) return SYSID_E_DEVICE;
   hipLaunchKernelGGL(xchg_unpack, dim3((unsigned)(((int64_t)n * n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), d_x, n, d_gram);
   return hipGetLastError() == hipSuccess ? SYSID_OK : SYSID_E_DEVICE;
-}
-
-int32_t sysid_set_fusion(sysid_engine* e, int32_t on) {
-  if (!e) return set_err(nullptr, SYSID_E_INVALID, "null engine");
-  e->fuse = on ? 1 : 0;
-  return SYSID_OK;
-}
-
-int32_t sysid_fused(const sysid_engine* e, uint32_t flags) {
-  if (!e) return SYSID_E_INVALID;
-  if (flags & (SYSID_EMIT_Y | SYSID_EMIT_TAU | SYSID_EMIT_FRICTION))
-    return k12_active(e, flags | SYSID_EMIT_GRAM, e->ldp) ? 1 : 0;
-  return gram_prec(flags) == 0 && e->k12_ok && e->fuse && !gram_nullspace(e, flags) ? 1 : 0;  // Gram-only
 }
 
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4) {

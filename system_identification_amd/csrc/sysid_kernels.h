@@ -22,7 +22,6 @@ constexpr int JT_FREEFLYER = 1;
 constexpr int JT_REVOLUTE = 2;
 constexpr int K1_WAVES = 4;            // waves (= samples in flight) per K1 workgroup
 constexpr int K1_SHARDS = 8;           // K1 sample ranges / claim counters (one per XCD), 128 B apart
-constexpr int K12_GW = 4;              // Gram waves per fused K1 + Gram workgroup (k12_fused_panel_gram)
 
 // ------------------------------------------------------------------------------------------------
 // layouts shared by host and device
@@ -159,9 +158,6 @@ struct K1Params {
   double thr_rel2;  // thr_rel^2, formed on the host (a kernel argument stays in SGPRs; the product hoisted out of the
                     // sample loop took a VGPR pair, which the register-bound kernels spilled)
   double g0, g1, g2;  // gravity (a_gf[0] = -gravity)
-  // the fused kernel's waits (k12_fused_panel_gram): a wait gives up after 2^k12_spin_log2 polls (~1 s at 23);
-  // k12_stall_polls > 0 (tests only) holds every Gram wave back that many polls before its first pair
-  int k12_spin_log2, k12_stall_polls;
 };
 constexpr int K1_QUAD_IN_MAX = 96;  // input channels of the quadruped K1 (nv = 18, two samples per wave)
 
@@ -512,26 +508,17 @@ constexpr int K1_QF_KMAX = 6;
 // Register-resident Gram-Schmidt of the runtime-nv kernels: at most 8 rows (one 8-lane group each) of nv <= 8 x
 // K1_MGS_NU entries (G1: 35); larger models take the LDS form (mgs_lds)
 constexpr int K1_MGS_NU = 5;
-// K1's per-wave body, shared by the standalone K1 (k1_regressor_panel, FUSED = 0: samples claimed from device
-// counters) and the K1 waves of the fused kernel (k12_fused_panel_gram, FUSED = 1: the workgroup's sample range
-// [f0, f1) dealt statically, wave w taking steps w, w + K1_WAVES, ...; after each step's panel stores have
-// completed the wave publishes its step count in k12_ready[w] (LDS) for the Gram waves of its workgroup).
-// FUSED = 2 (the fused Gram-only mode): `panel` is the wave's ring of k12_ring steps; step t's rows go to slot
-// t % k12_ring once EVERY Gram wave has completed its loads of step t - k12_ring (k12_consumed[g] = the pairs Gram
-// wave g has finished, in order).
-template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0, int FUSED = 0>
+// K1's per-wave body (k1_regressor_panel): samples claimed from device counters.
+template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0>
 __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __restrict__ mimg_g,
                                         const double* __restrict__ in, int64_t N, int64_t ld,
                                         OutT* __restrict__ panel, int64_t ldp, unsigned long long* __restrict__ work,
-                                        double* __restrict__ dbg, int* __restrict__ rcount, int* k12_ready,
-                                        int64_t f0, int64_t f1, int* k12_consumed = nullptr,
-                                        int k12_ring = 0) {
+                                        double* __restrict__ dbg, int* __restrict__ rcount) {
   static_assert(!(POV && CMP), "the nullspace mode runs the plain layout");
   static_assert(!QF || (NVC == 0 && !POV && !CMP), "the Q-form is a runtime-nv, plain-layout kernel");
-  static_assert(!FUSED || (!CMP && !POV && !QF), "the fused kernel runs the plain projector-row layout");
   extern __shared__ double smem[];
   const MImg MI = mimg_layout(kp.NJ, kp.nv, kp.nc, kp.maxch);
-  if constexpr (!FUSED) {
+  {
     uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
     for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
     __syncthreads();  // the only workgroup barrier: the model image is read-only from here on
@@ -595,10 +582,8 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   const int home = (int)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (K1_SHARDS - 1));  // XCC_ID
   auto shard_begin = [&](int x) -> int64_t { return k1_shard_begin(N, x); };
   int sh = 0;  // shards (counted from home) found exhausted by this wave
-  int64_t fnext = f0 + (int64_t)SPW * wave;  // FUSED: the wave's next step in the static deal
   auto claim_issue = [&]() -> unsigned long long {
     unsigned long long v = 0;
-    if constexpr (FUSED) return v;
     if (lane == 0) {
       // an opaque (per-lane) offset keeps the atomic optimizer from rewriting the claim as a wave scan,
       // which reads the returned value (and waits for it) right at the atomic
@@ -616,11 +601,6 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   // the sample of a claim issued on the current shard, or (that shard exhausted) the next claim that succeeds
   // on the following shards, or N when every shard is exhausted
   auto claim_value = [&](unsigned long long raw) -> int64_t {
-    if constexpr (FUSED) {
-      const int64_t v = fnext;
-      fnext += (int64_t)SPW * K1_WAVES;
-      return v < f1 ? v : N;
-    }
     unsigned long long v = uniform64(raw);
     bool have = true;  // v is a claim on shard (home + sh)
     while (sh < K1_SHARDS) {
@@ -679,13 +659,6 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   // issues first when its operands arrive (K1 -1 to -2%, Spot and G1)
   __builtin_amdgcn_s_setprio(2);
   const int hl_outer = hl;
-  int steps_done = 0;  // FUSED: steps whose panel stores have completed are published
-  auto publish = [&](int n) {
-    if constexpr (FUSED) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's panel stores have reached L2
-      if (lane == 0) __hip_atomic_store(k12_ready + wave, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  };
   while (s < N) {
     // Quadruped variant (OPQ): the lane index and the per-sample LDS region are re-derived opaquely every
     // step, so the per-lane index arithmetic of the phase loops (nv is a compile-time constant) and the
@@ -1501,43 +1474,12 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     wsync();
     if (s1 < N) commit();
     wsync();
-    // the previous step's stores were issued before this step's input prefetch, which commit() has just waited
-    // for: publishing them here costs no extra wait
-    if (steps_done > 0) publish(steps_done);
-
-    if constexpr (FUSED == 2) {
-      // The ring slot this step overwrites held step steps_done - k12_ring, i.e. pair 4 (steps_done - k12_ring) + wave of
-      // the workgroup: EVERY Gram wave must have completed its loads of it.  Each Gram wave g counts its own finished
-      // pairs (k12_consumed[g], in pair order), and the wait is on each of them: a sum over the Gram waves (round 4)
-      // let a leading wave's count cover a lagging one that had not read the slot yet.  The wait is bounded (a bug must
-      // not hang the device): when it gives up, the workgroup's abort word (after the counters) is set before the slot
-      // is overwritten, so the Gram waves poison their tiles with NaN, and every later wait returns at once.
-      int* abort_word = k12_consumed + K12_GW;
-      const int need = (steps_done - k12_ring) * K1_WAVES + wave + 1;  // pairs every Gram wave must have finished
-      if (steps_done >= k12_ring) {
-        int spins = 0;
-        for (int g = 0; g < K12_GW; ++g) {
-          while (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
-                 __hip_atomic_load(k12_consumed + g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-            if (++spins >= (1 << kp.k12_spin_log2)) {
-              if (lane == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the abort word is in LDS before the ring store
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-      }
-    }
     __builtin_amdgcn_s_setprio(0);
     // ---- projected regressor Y_proj: lane = (body i, row group g), all ten columns of body i ----
     // Y_proj[r, block i] = G_i[r, :] F_i with G_i = P[:, ff] J_w[:, ff]^T + sum over the revolute
     // chain of i of P[:, d] J_w[:, d]^T (= H1 + ...), F_i the body's world-frame regressor block.
     // One G row (6 + 6*chain FMAs) feeds 42 FMAs.
-    // the step's rows: the stacked panel's, or (fused Gram-only) the ring slot of this step
-    OutT* const obase = FUSED == 2 ? panel + (int64_t)((steps_done % (k12_ring > 0 ? k12_ring : 1)) * SPW) * nv * ldp
-                                   : panel + s * nv * ldp;
-    OutT* out = FUSED ? obase + (int64_t)half * nv * ldp : panel + ((s + half) * nv) * ldp;
+    OutT* out = panel + ((s + half) * nv) * ldp;
     const int nbody = NJ - 1, nyi = nbody * kp.rg;
     auto block_row = [&](int r, const double* F, const int* dof, int cl, double* y) {
       const double* h = h1_in_p ? Ps + r * nv + kp.ff0 : H1 + 6 * r;
@@ -1624,7 +1566,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       // 2x, plus dg for the second group.  The row start of the wave's first sample is wave-uniform (scalar
       // registers); the second sample's rows and the column go into a 32-bit lane byte offset, so each store is
       // a scalar-base + lane-offset store with no 64-bit address math.
-      char* ybase = reinterpret_cast<char*>(FUSED ? obase : panel + (s * NVC) * ldp);
+      char* ybase = reinterpret_cast<char*>(panel + (s * NVC) * ldp);
       const uint32_t yhoff = (uint32_t)(half * NVC * (int)ldp * (int)sizeof(OutT));
       const int dg = rh * (int)ldp - kp.wy;
       // Rows in pairs with two explicit H1 / P register sets (no copies between them): row rho + 1's LDS reads
@@ -2057,9 +1999,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     __builtin_amdgcn_s_setprio(2);
     s = s1;
     s1 = s2;
-    ++steps_done;
   }
-  publish(steps_done);
 }
 
 template <int MAXCH, int NVC, int SPW, typename OutT, int POV = 0, int CMP = 0, int QF = 0>
@@ -2070,237 +2010,7 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
                    int64_t N, int64_t ld, OutT* __restrict__ panel, int64_t ldp,
                    unsigned long long* __restrict__ work, double* __restrict__ dbg,
                    int* __restrict__ rcount) {
-  k1_body<MAXCH, NVC, SPW, OutT, POV, CMP, QF, 0>(kp, mimg_g, in, N, ld, panel, ldp, work, dbg, rcount, nullptr, 0,
-                                                  0);
-}
-
-// ------------------------------------------------------------------------------------------------
-// K12: K1 and the Gram in one launch (narrow Grams of 10 tile columns fed by the quadruped K1: Spot, Solo-12).
-//
-// K1 is VALU / LDS bound at two waves per SIMD and K2 is MFMA bound; run one after the other they use one pipe
-// at a time.  Here every workgroup (one per CU) holds 4 K1 waves and 4 Gram waves, one of each per SIMD, and the
-// SIMD's VALU and matrix pipes run side by side (MI355X_MICROARCH.md, "MFMA and VALU pipes are separate").
-// The samples are dealt statically: workgroup b takes the sample pairs [P b / G, P (b+1) / G), its K1 wave w the
-// pairs w, w + 4, ... of that range (k1_body, FUSED = 1), writing the stacked panel to HBM as the standalone K1
-// does.  A K1 wave publishes, in LDS, how many of its steps have completed (their stores acknowledged by L2:
-// s_waitcnt vmcnt(0)); the Gram waves walk the workgroup's pairs in order and read each pair's 36 rows back from
-// L2 as MFMA fragments (nontemporal loads), accumulating their
-// tiles in registers: no LDS staging, no barrier, and no re-read of the panel from HBM.  Each Gram wave owns a
-// fixed set of the Gram's 55 upper 16x16 tiles (k12_role: block columns paired high with low, 14/14/14/13
-// tiles) and writes them to its workgroup's slab once at the end; K3 sums the slabs as after K2.
-// Deterministic: the deal, the pair order and every accumulation order are fixed.
-// No Gram wave waits on anything but its own workgroup's K1 waves, which never wait on it, so the launch cannot
-// deadlock; a wait still gives up after ~1 s and poisons its tiles with NaN (a bug must not hang the GPU).
-// ------------------------------------------------------------------------------------------------
-constexpr int K12_NTC = 10;
-constexpr int K12_NSLOTS = 55;   // upper tiles of a 10 x 10 tile Gram
-struct K12Role {
-  int nc;        // tile columns of the role
-  int col[4];    // their block column J
-  int nrow[4];   // tiles (I = 0 .. nrow - 1) of each
-  int base;      // first slab slot
-  int ntiles;
-};
-__host__ __device__ constexpr K12Role k12_role(int w) {
-  return w == 0 ? K12Role{2, {9, 3, 0, 0}, {10, 4, 0, 0}, 0, 14}
-       : w == 1 ? K12Role{2, {8, 4, 0, 0}, {9, 5, 0, 0}, 14, 14}
-       : w == 2 ? K12Role{2, {7, 5, 0, 0}, {8, 6, 0, 0}, 28, 14}
-                : K12Role{4, {6, 2, 1, 0}, {7, 3, 2, 1}, 42, 13};
-}
-// slab slot -> (I, J) block coordinates (host: the K3 tile table; device: the fragments of a tile)
-__host__ __device__ constexpr int2 k12_tile(int slot) {
-  int w = 3;
-  while (w > 0 && k12_role(w).base > slot) --w;
-  const K12Role R = k12_role(w);
-  int t = slot - R.base;
-  for (int c = 0; c < R.nc; ++c) {
-    if (t < R.nrow[c]) return int2{t, R.col[c]};
-    t -= R.nrow[c];
-  }
-  return int2{-1, -1};
-}
-
-// RING = 0: the pairs are rows of the stacked panel; RING > 0 (fused Gram-only): pair p of the workgroup is slot
-// (p / 4) % RING of K1 wave p % 4's ring, and once its loads are complete k12_consumed[W] (this Gram wave's count of
-// finished pairs) becomes p + 1.
-template <int W, int NVC, int RING>
-__device__ __forceinline__ void k12_gram_wave(const double* __restrict__ panel, int64_t ldp, int64_t N, int64_t f0,
-                                              int64_t f1, const int* k12_ready, double* __restrict__ slab,
-                                              int* k12_consumed, int spin_log2, int stall_polls) {
-  constexpr K12Role R = k12_role(W);
-  constexpr int NB = R.col[0] + 1;         // fragment blocks 0 .. col[0] (every role's first column is its widest)
-  constexpr int NT = R.ntiles;
-  constexpr int KSP = (2 * NVC + 3) / 4;   // k-steps (4 rows) per pair of samples
-  static_assert(KSP == 9, "the unit schedule below is written for 36-row pairs");
-  const int lane = threadIdx.x & 63, kr = lane >> 4, kc = lane & 15;
-  const int64_t np = (f1 - f0 + 1) / 2;
-  dbl4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
-  bool bad = false;
-  int* abort_word = k12_consumed + K12_GW;  // set by any wave of the workgroup whose wait gave up
-  for (int x = 0; x < stall_polls; ++x) __builtin_amdgcn_s_sleep(2);  // tests: force the K1 waves' waits to expire
-  // a pair is ready once its K1 wave (pair % 4) has published step pair / 4
-  auto wait_pair = [&](int64_t p) {
-    const int v = (int)(p & (K1_WAVES - 1)), need = (int)(p / K1_WAVES) + 1;
-    int spins = 0;
-    while (__hip_atomic_load(k12_ready + v, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-      if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) {
-        bad = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins >= (1 << spin_log2)) {  // ~1 s: never expected; give up rather than hang the device
-        bad = true;
-        if (lane == 0) __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        break;
-      }
-    }
-  };
-  // Loads are unconditional (a masked load became an exec-masked branch with its own vmcnt(0) wait), at
-  // immediate offsets 16 b from one row address.  Lanes of the last block whose column is past the row
-  // (16 b + kc >= ldp) read the row's last column instead of the next row's first ones: what they add lands only
-  // in Gram entries past column ldp - 1, which K3 never writes, and no load leaves the pair's rows.  The K1 stores
-  // and these loads run on one CU (one L1, one L2): the workgroup-scope acquire of the ready count orders them.
-  // The panel's last pair and an odd last sample run the clamped, zero-scaled loads.
-  auto ld_nt = [](const double* p) { return __builtin_nontemporal_load(p); };
-  const int clast = 16 * (NB - 1) + kc < ldp ? 16 * (NB - 1) : (int)ldp - 1 - kc;  // the last block's column
-  auto pair_base = [&](int64_t p, const double*& base, int& nrows) {
-    const int64_t s0 = f0 + 2 * p;
-    nrows = (f1 - s0 >= 2 ? 2 : 1) * NVC;
-    if constexpr (RING > 0) {
-      const int64_t slot = ((int64_t)blockIdx.x * K1_WAVES + (p & (K1_WAVES - 1))) * RING + (p / K1_WAVES) % RING;
-      base = panel + (slot * 2 * NVC + kr) * ldp + kc;
-    } else {
-      base = panel + (s0 * NVC + kr) * ldp + kc;  // this lane's row of the pair's first k-step
-    }
-  };
-  // ring mode: pair p's loads have all returned (the ones issued after them: `younger`) -> its slot may be reused
-  auto consumed = [&](int64_t p, auto younger) {
-    if constexpr (RING > 0) {
-      constexpr int Y = decltype(younger)::value;
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Y) : "memory");
-      if (lane == 0) __hip_atomic_store(k12_consumed + W, (int)(p + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    (void)p;
-  };
-  auto issue = [&](const double* base, int k, double (&f)[NB]) {
-    const double* rowp = base + (int64_t)(4 * k) * ldp;
-#pragma unroll
-    for (int b = 0; b < NB - 1; ++b) f[b] = ld_nt(rowp + 16 * b);
-    f[NB - 1] = ld_nt(rowp + clast);
-  };
-  auto issue_edge = [&](const double* base, int nrows, int k, double (&f)[NB]) {
-    const int r = 4 * k + kr;
-    const bool rok = r < nrows;
-    const double rs = rok ? 1.0 : 0.0;
-    const double* rowp = base + (int64_t)((rok ? r : kr) - kr) * ldp;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int c = 16 * b + kc < ldp ? 16 * b : (int)ldp - 1 - kc;
-      f[b] = ld_nt(rowp + c) * rs;
-    }
-  };
-  auto mma = [&](const double (&f)[NB]) {
-    int t = 0;
-#pragma unroll
-    for (int c = 0; c < R.nc; ++c)
-#pragma unroll
-      for (int i = 0; i < R.nrow[c]; ++i) {
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[i], f[R.col[c]], acc[t], 0, 0, 0);
-        ++t;
-      }
-  };
-  // Nine units (k-steps) per pair, three fragment sets in rotation: unit k + 2 is requested while unit k is
-  // multiplied, across pair boundaries (the last two units of pair p request the first two of pair p + 1).  The
-  // pipelined loop runs the workgroup's whole pairs with plain loads; the panel's last pair (the workgroup with
-  // f1 == N) and an odd last sample run after it, unit by unit, with the clamped loads.
-  const int64_t nfull = (f1 - f0) / 2;
-  const int64_t nfast = f1 >= N && nfull > 0 ? nfull - 1 : nfull;
-  double fa[NB], fb[NB], fc[NB];
-  const double* cb = panel;
-  int cn = 0;
-  if (nfast > 0) {
-    wait_pair(0);
-    pair_base(0, cb, cn);
-    issue(cb, 0, fa);
-    issue(cb, 1, fb);
-  }
-  for (int64_t p = 0; p < nfast && !bad; ++p) {
-    issue(cb, 2, fc); mma(fa);
-    issue(cb, 3, fa); mma(fb);
-    issue(cb, 4, fb); mma(fc);
-    issue(cb, 5, fc); mma(fa);
-    issue(cb, 6, fa); mma(fb);
-    issue(cb, 7, fb); mma(fc);
-    issue(cb, 8, fc); mma(fa);
-    const bool more = p + 1 < nfast;
-    if (more) {
-      wait_pair(p + 1);
-      pair_base(p + 1, cb, cn);
-      issue(cb, 0, fa);
-    }
-    mma(fb);
-    if (more) issue(cb, 1, fb);
-    mma(fc);
-    if (more) consumed(p, std::integral_constant<int, 2 * NB>{});
-    else consumed(p, std::integral_constant<int, 0>{});
-  }
-  for (int64_t p = nfast; p < np && !bad; ++p) {
-    wait_pair(p);
-    pair_base(p, cb, cn);
-    for (int k = 0; k < KSP; ++k) {
-      issue_edge(cb, cn, k, fa);
-      mma(fa);
-    }
-    consumed(p, std::integral_constant<int, 0>{});
-  }
-  // a K1 wave that gave up overwrote a ring slot that may not have been read: the tiles are poisoned too
-  if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) bad = true;
-  double* o = slab + ((size_t)blockIdx.x * K12_NSLOTS + R.base) * 256;
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[t * 256 + (kr + 4 * j) * 16 + kc] = bad ? __builtin_nan("") : acc[t][j];
-}
-
-// RING = 0: full outputs (`panel` = the stacked panel); RING > 0: Gram-only (`panel` = the rings, gridDim.x x
-// K1_WAVES x RING slots of 2 nv rows, plus one row of slack for the last row's over-read).
-template <int MAXCH, int NVC, int SPW, int RING>
-__global__ void __launch_bounds__(64 * (K1_WAVES + K12_GW), 2)
-k12_fused_panel_gram(const K1Params kp, const uint32_t* __restrict__ mimg_g, const double* __restrict__ in,
-                     int64_t N, int64_t ld, double* __restrict__ panel, int64_t ldp, double* __restrict__ slab) {
-  static_assert(NVC == 18 && SPW == 2, "the fused kernel serves the quadruped K1 (two samples per wave)");
-  extern __shared__ double smem[];
-  int* ready = reinterpret_cast<int*>(smem + kp.mimg_dbl + K1_WAVES * SPW * kp.wave_dbl);
-  int* consumed = ready + K1_WAVES;
-  {
-    uint32_t* mw = reinterpret_cast<uint32_t*>(smem);
-    for (int x = threadIdx.x; x < 2 * kp.mimg_dbl; x += blockDim.x) mw[x] = mimg_g[x];
-    if (threadIdx.x < K1_WAVES + K12_GW + 1) ready[threadIdx.x] = 0;  // ready[4], consumed[4], abort word
-  }
-  __syncthreads();
-  const int64_t P = (N + SPW - 1) / SPW;
-  const int64_t p0 = P * blockIdx.x / gridDim.x, p1 = P * (blockIdx.x + 1) / gridDim.x;
-  const int64_t f0 = p0 * SPW, f1 = p1 * SPW < N ? p1 * SPW : N;
-  const int wave = threadIdx.x >> 6;
-  if (wave < K1_WAVES) {
-    if constexpr (RING > 0) {
-      double* ring = panel + ((int64_t)blockIdx.x * K1_WAVES + wave) * RING * SPW * NVC * ldp;
-      k1_body<MAXCH, NVC, SPW, double, 0, 0, 0, 2>(kp, mimg_g, in, N, ld, ring, ldp, nullptr, nullptr, nullptr, ready,
-                                                   f0, f1, consumed, RING);
-    } else {
-      k1_body<MAXCH, NVC, SPW, double, 0, 0, 0, 1>(kp, mimg_g, in, N, ld, panel, ldp, nullptr, nullptr, nullptr,
-                                                   ready, f0, f1);
-    }
-  } else {
-    switch (wave - K1_WAVES) {
-      case 0: k12_gram_wave<0, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
-      case 1: k12_gram_wave<1, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
-      case 2: k12_gram_wave<2, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
-      default: k12_gram_wave<3, NVC, RING>(panel, ldp, N, f0, f1, ready, slab, consumed, kp.k12_spin_log2, kp.k12_stall_polls); break;
-    }
-  }
+  k1_body<MAXCH, NVC, SPW, OutT, POV, CMP, QF>(kp, mimg_g, in, N, ld, panel, ldp, work, dbg, rcount);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -33,14 +33,6 @@ void k1_launch(int variant, dim3 g, dim3 b, size_t lds, hipStream_t st, const sy
                const uint32_t* mimg, const double* d_in, int64_t N, int64_t ld, void* d_panel, int64_t ld_panel,
                unsigned long long* work, double* dbg, int* rcount);
 
-// The fused K1 + Gram kernel (k12_fused_panel_gram) of K1_C4_NV18 (f64 panel): one workgroup of K1_WAVES +
-// K12_GW waves per CU; `slab` holds gridDim.x x K12_NSLOTS tiles for K3.  ring = 0: full outputs (d_panel = the
-// stacked panel); ring = 1: Gram-only, d_panel = the per-wave rings of K12_RING two-sample slots.
-constexpr int K12_RING = 3;
-const void* k12_fn(int ring);
-void k12_launch(int ring, dim3 g, size_t lds, hipStream_t st, const sysid_dev::K1Params& kp, const uint32_t* mimg,
-                const double* d_in, int64_t N, int64_t ld, double* d_panel, int64_t ld_panel, double* slab);
-
 // One K2 launch: the Gram's tile columns, the deal (super-tile / tile-slot table of the arithmetic), the split
 // and the rows (gathered through rowlist / d_rows in the nullspace mode).
 struct K2Args {

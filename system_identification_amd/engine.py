@@ -61,8 +61,6 @@ SIGNATURES = [
     ("sysid_gram_rows", _c.c_int32, [_vp, _c.c_uint32]),
     ("sysid_set_gram_chunk_bytes", _c.c_int32, [_vp, _c.c_uint64]),
     ("sysid_debug_k2_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
-    ("sysid_set_fusion", _c.c_int32, [_vp, _c.c_int32]),
-    ("sysid_fused", _c.c_int32, [_vp, _c.c_uint32]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
@@ -394,17 +392,6 @@ class Engine:
         """Chunk panel size of the Gram-only path (>= 1 MiB; 0 = the 4 GiB default).  alloc_gram_device /
         gram_workspace_bytes follow it, so set it before allocating."""
         self._check(self.lib.sysid_set_gram_chunk_bytes(self._h, int(nbytes)))
-
-    def set_fusion(self, on: bool) -> None:
-        """Fused K1 + Gram for the quadrupeds' f64 Grams (sysid_set_fusion; off by default: measured slower)."""
-        self._check(self.lib.sysid_set_fusion(self._h, 1 if on else 0))
-
-    def fused(self, flags: int = EMIT_ALL) -> bool:
-        """Whether these flags run the fused K1 + Gram kernel: with a stacked-output flag build_device (and the
-        engine's panel ld), without one build_gram_device."""
-        if not hasattr(self.lib, "sysid_fused"):
-            return False  # an older A/B build
-        return self.lib.sysid_fused(self._h, int(flags)) == 1
 
     def gram_rows(self, precision: str = "f64", rows: str = "auto") -> str:
         """The rows build_gram_device uses: "nullspace" (Zᵀ·A) or "projector" (P·A)."""

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors_without_gpu():
     lib = engine.load_library()
-    assert lib.sysid_abi_version() == 7
+    assert lib.sysid_abi_version() == 8
     out = ctypes.c_void_p()
     rc = lib.sysid_model_create(b"\x00" * 8, 8, 0, ctypes.byref(out))
     assert rc == engine.SYSID_E_MODEL and not out.value

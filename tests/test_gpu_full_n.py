@@ -73,7 +73,7 @@ def test_whole_panel_and_gram_vs_oracle(robot, N, cfg):
         "B_c": block_errors(P[:, wy + nj:W], o["B_c"], N, nv, FLOOR),
     }
     worst = {k: (float(v.max()), int(v.argmax())) for k, v in errs.items()}
-    print(f"{robot} {N} (fused: {e.fused(EMIT_ALL)}): oracle {t_o:.2f} s on 16 threads; worst block "
+    print(f"{robot} {N}: oracle {t_o:.2f} s on 16 threads; worst block "
           + ", ".join(f"{k} {v[0]:.1e} (sample {v[1]})" for k, v in worst.items()))
     for k, (v, s) in worst.items():
         assert v < TOL, (k, s, v)

@@ -1,5 +1,4 @@
-"""Per-kernel HIP-event times of one library build over several workloads (dev tool; SYSID_LIB selects the build,
-SYSID_AB_FUSE=1 turns the fused K1 + Gram kernel on):
+"""Per-kernel HIP-event times of one library build over several workloads (dev tool; SYSID_LIB selects the build):
 spot 20k full outputs, spot 20k Gram-only f64 (engine's rows), g1 20k full outputs, g1 125k Gram-only bf16.
 usage: SYSID_LIB=<lib> python tools/ab_kernels.py [workload ...]"""
 import os
@@ -20,8 +19,6 @@ for name in names:
     robot, N, prec = WL[name]
     m = load_robot(robot)
     e = Engine(m)
-    if os.environ.get("SYSID_AB_FUSE") == "1":
-        e.set_fusion(True)  # the fused K1 + Gram kernel where the model has it (time_stages: K1 slot = K12)
     d = generate(m, N, 1)
     din = torch.from_numpy(channel_block(d)).cuda()
     if prec is None:
