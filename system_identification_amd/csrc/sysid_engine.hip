@@ -137,6 +137,7 @@ struct sysid_engine {
   };
   K1Shape k1m[3];  // projector rows, per panel element type (0 f64 / every stacked output, 1 f32, 2 bf16)
   K1Shape k1c[3];  // the Gram-only nullspace mode (CMP instantiations of the plain layout), per element type
+  K1Shape k1f;     // the full-force mode (sysid_build_full): k1m[0], or K1_C4 where k1m[0] is the quadruped kernel
   int k1_maxch_tpl = 4;
   // K2/K3 Gram tiling
   int ntc = 0;
@@ -255,10 +256,12 @@ bool k1_is_pov(int variant) { return variant == K1_C12P || variant == K1_C16P; }
 int k1_chain_slots(int maxch) { return maxch <= 4 ? 4 : maxch <= 12 ? 12 : 16; }
 
 // maxch: the longest revolute chain.  The nv = 18 kernel unrolls SYSID_K1_QCH chain slots.
-int k1_variant(int maxch, int nv, int nbody, int in_lds) {
-  // the nv = 18 kernel stages two panel rows of all bodies (lane = body x row group: 11..16 bodies) and prefetches
-  // at most K1_QUAD_IN_MAX input channels (its registers are sized for them)
-  if (maxch <= SYSID_K1_QCH && nv == 18 && nbody >= 11 && nbody <= 16 && in_lds <= K1_QUAD_IN_MAX) return K1_C4_NV18;
+int k1_variant(int maxch, int nv, int nbody, int in_lds, int nc) {
+  // the nv = 18 kernel stages two panel rows of all bodies (lane = body x row group: 11..16 bodies), prefetches at
+  // most K1_QUAD_IN_MAX input channels (its registers are sized for them) and keeps J_c's rows in lane pairs (3 nc
+  // rows in 32 lanes: at most 5 contact frames)
+  if (maxch <= SYSID_K1_QCH && nv == 18 && nbody >= 11 && nbody <= 16 && in_lds <= K1_QUAD_IN_MAX && 6 * nc <= 32)
+    return K1_C4_NV18;
   return maxch <= 4 ? K1_C4 : k1_chain_slots(maxch) == 12 ? K1_C12 : K1_C16;
 }
 
@@ -306,7 +309,7 @@ int launch_k1(sysid_engine* e, const double* d_in, int64_t N, int64_t ld, void* 
     kp.full = 1;
     kp.in_rows = e->in_lds;
   }
-  const sysid_engine::K1Shape& K = cmp ? e->k1c[prec] : e->k1m[full ? 0 : prec];
+  const sysid_engine::K1Shape& K = cmp ? e->k1c[prec] : full ? e->k1f : e->k1m[prec];
   const int variant = K.variant, waves = K.waves, bpc = K.bpc;
   const size_t lds = K.lds;
   kp.pov = K.pov;
@@ -959,7 +962,7 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   e->ldp = (e->ncol + 1) & ~1;
   e->in_rows = in_rows;
   e->in_lds = in_lds;
-  const int v0 = k1_variant(maxch, nv, NJ - 1, in_lds);
+  const int v0 = k1_variant(maxch, nv, NJ - 1, in_lds, nc);
   const int lhw = k1_layout_hw(v0);
   const WLay WL0 = wave_layout(in_lds, nv, NJ, nc, lhw);
   // P overlay (wave_layout `pov`): runtime-nv kernels whose H1 is read from P (an even free-flyer offset), when
@@ -1188,6 +1191,14 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
       }
       const int z1[1] = {0};
       if (ok) ok = shape(e->k1c[pr], pr, 1, &v0, &WL0, z1, z1, 1);
+    }
+    // the full-force mode: the quadruped kernel has none (its instantiation drops the mode's paths), so those models
+    // run it on the generic 4-slot kernel with the plain layout
+    e->k1f = e->k1m[0];
+    if (ok && v0 == K1_C4_NV18) {
+      const int vf[1] = {sysid_launch::K1_C4}, z1[1] = {0};
+      const WLay WLF = wave_layout(in_lds, nv, NJ, nc, 0);
+      ok = shape(e->k1f, 0, 0, vf, &WLF, z1, z1, 1);
     }
     if (!ok) {
       set_err(nullptr, SYSID_E_MODEL, "model needs too much LDS per sample (%zu B)", (size_t)WL0.total * 8);

@@ -49,8 +49,9 @@ void k2_case(const K2Args& a) {
         hipLaunchKernelGGL((k2_gram_syrk_dma<E, NTC, DKC>), g2, b2, 0, a.st, P, a.rows, a.ld_panel, T, a.ngroups,
                            a.ks, a.nslots, a.accumulate, a.slab, nullptr, nullptr);
     } else if (gather) {
-      hipLaunchKernelGGL((k2_gram_syrk_dma<E, NTC, DKC, true>), g2, b2, 0, a.st, P, a.rows, a.ld_panel, T,
-                         a.ngroups, a.ks, a.nslots, a.accumulate, a.slab, a.rowlist, a.d_rows);
+      constexpr int RKC = (PREC == 0 ? 1 : 2) * KC;
+      hipLaunchKernelGGL((k2_gram_syrk_gather<E, NTC, RKC>), g2, b2, 0, a.st, P, a.rows, a.ld_panel, T, a.ngroups,
+                         a.ks, a.nslots, a.accumulate, a.slab, a.rowlist, a.d_rows);
     } else {
       constexpr int RKC = (PREC == 0 ? 1 : 2) * KC;
       hipLaunchKernelGGL((k2_gram_syrk<E, NTC, RKC>), g2, b2, 0, a.st, P, a.rows, a.ld_panel, T, a.ngroups, a.ks,

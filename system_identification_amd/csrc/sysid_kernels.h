@@ -543,6 +543,9 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
   const double* ct = smem + MI.ct;
 
   const int nv = NVC > 0 ? NVC : kp.nv;
+  // the quadruped kernel carries no full-force mode (the engine runs that mode on the K1_C4 instantiation): its dead
+  // paths cost the kernel registers (SGPR spills) and code
+  const int kfull = NVC == 18 ? 0 : kp.full;
   const int nq = kp.nq, nc = kp.nc, NJ = kp.NJ, bd = kp.bd, nja = kp.nj, IN = kp.in_rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   static_assert(SPW == 1 || SPW == 2, "1 or 2 samples per wave (4 measured 34% slower)");
@@ -967,7 +970,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     // in place (an even ff0 keeps the rows' 16-byte alignment); otherwise H1 is copied out below.
     const bool h1_in_p = kp.has_ff && (kp.ff0 & 1) == 0;
     int nrows = nv;  // output rows of the sample: nv, or nv - rank(J_c) in the nullspace mode (CMP)
-    if (kp.full) {
+    if (kfull) {
       // get_full_regressor_force (src/sys_identification.py:391-399): no projection.  With the overlay P = I
       // is written after the tau column below (which reads J_c, under P's slot there).
       if constexpr (!POV && !QF) {
@@ -1054,7 +1057,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         }
       };
       if constexpr (NVC == 18 && HW == 32) {
-        if (2 * k <= HW) {
+        {  // 2k <= HW: the engine picks this kernel for at most 5 contact frames (k <= 15)
           // Quadruped form: lane pair (2j, 2j+1) keeps its half-row of row j in registers through every
           // step; the pivot's norm comes from its lanes by readlane (no LDS round trip per step) and only
           // the pivot's half-row is read from LDS; an updated row is written back for its own turn.
@@ -1116,8 +1119,6 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             if (CMP && h == 0) nrm[j] = -sc;  // taken rows < 0, as in mgs_lds (read by the nullspace phase)
           }
           wsync();
-        } else {
-          mgs_lds();
         }
       } else if (8 * k <= HW && nv <= 8 * K1_MGS_NU) {
         // Runtime-nv form for at most HW / 8 rows and nv <= 40 (G1: k <= 6, nv = 35): lane group j (8 lanes) keeps row
@@ -1387,7 +1388,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     // tp first: in the full mode H1 may be stored over J_c (overlay layout), which the tau column reads.
     // Q-form: tp = S^T tau - Qᵀ u, u_j = Q_j · S^T tau (u in the dead row-norm slots)
     if constexpr (QF) {
-      if (!kp.full) {
+      if (!kfull) {
         // u_j = Q_j . S^T tau: eight lanes per row j (k <= K1_QF_KMAX <= 8 rows, whole 8-lane groups active), each
         // summing every eighth joint, then a DPP sum over the group — not one lane per row walking all nj joints
         // (a 29-long chain of dependent LDS reads on G1)
@@ -1404,7 +1405,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     }
     for (int r = hl; r < nrows; r += HW) {
       double acc = 0.0;
-      if ((POV || QF) && kp.full) {
+      if ((POV || QF) && kfull) {
         acc = r >= bd && r < bd + nja ? tau[r - bd] : 0.0;  // P = I (not yet written)
       } else if constexpr (QF) {
         acc = r >= bd && r < bd + nja ? tau[r - bd] : 0.0;
@@ -1413,7 +1414,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
 #pragma unroll 4
         for (int jj = 0; jj < nja; ++jj) acc += Ps[r * nv + bd + jj] * tau[jj];
       }
-      if (kp.full) {
+      if (kfull) {
         // + J_c^T lambda, lambda = the measured forces of the feet in contact in foot order, world axes
         // (LOCAL_WORLD_ALIGNED).  J_c here is in base axes, J_c,world = R_b J_c, so lambda is moved to
         // base axes with R_b^T (R_b = the base quaternion's matrix, unnormalised like pinocchio's).
@@ -1438,8 +1439,8 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       }
       tps[r] = acc;
     }
-    if (kp.full && !POV) wsync();
-    if (POV && kp.full) {
+    if (kfull && !POV) wsync();
+    if (POV && kfull) {
       wsync();  // J_c read: P = I may overwrite it now
       for (int e = hl; e < nv * nv; e += HW) {
         const int a = e / nv;
@@ -1454,7 +1455,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     if constexpr (QF) {
       // Qt[r][j] = Q_j[r] (zero past the sample's k rows; in the full mode P = I: no rows), over the dead
       // W / Pt / contact-point slot: a row's K1_QF_KMAX entries are three 16-byte reads from one address
-      const int kq = kp.full ? 0 : k;
+      const int kq = kfull ? 0 : k;
       for (int e = hl; e < nv * K1_QF_KMAX; e += HW) {
         const int r = e / K1_QF_KMAX, j = e - K1_QF_KMAX * r;
         Qt[e] = j < kq ? Jc[j * nv + r] : 0.0;
@@ -1635,7 +1636,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       // (its three columns of K) and takes the other three from its partner by DPP; F6's columns are permuted
       // per lane to [own three | partner's three].  k is wave-uniform (one sample per wave): the row loop is
       // specialised for k <= 3 and k <= 6.
-      const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);
+      const int kq = __builtin_amdgcn_readfirstlane(kfull ? 0 : k);
       const int nyh = 2 * nbody;  // even: both lanes of a pair are always active together
       if constexpr (std::is_same_v<OutT, __bf16>) {
         float* q32w = reinterpret_cast<float*>(wr + L.q32);
@@ -1869,7 +1870,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
     // factors and column selects are fixed over its rows (Spot: 15 pairs, two 16-lane groups, 9 rows each);
     // otherwise lane = (row, column pair) with a division per item.
     const int npair = (kp.out_cols - kp.wy) >> 1;  // out_cols and wy are even
-    if (npair <= 32) {
+    if (NVC == 18 || npair <= 32) {
       const int lg = npair <= 8 ? 3 : (npair <= 16 ? 4 : 5);  // log2 of the group width
       const int NG = HW >> lg;
       const int fg = hl >> lg, m = hl & ((1 << lg) - 1);
@@ -1892,7 +1893,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
         const int64_t pstep = (int64_t)NG * ldp;
         if constexpr (QF) {
           // P[r, bd + j] = δ - Σ_i Q_i[r] Q_i[bd + j]: the lane's two columns of Q in registers
-          const int kq = __builtin_amdgcn_readfirstlane(kp.full ? 0 : k);  // wave-uniform (one sample per wave)
+          const int kq = __builtin_amdgcn_readfirstlane(kfull ? 0 : k);  // wave-uniform (one sample per wave)
           (void)kq;
           double qc[K1_QF_KMAX][2];
 #pragma unroll
@@ -1946,7 +1947,7 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             panel_store(po, v2[0], v2[1]);
           }
           }
-        } else if (NVC == 18 && HW == 32 && !CMP && NG == 2) {
+        } else if constexpr (NVC == 18 && HW == 32 && !CMP) {
           // Spot / Solo (13 column pairs: two 16-lane groups, 9 rows each): every row's LDS reads issued up front
           // instead of one wait per row of the rolled loop (Spot K1 -4%, profiles/r05_s4)
           constexpr int NR = NVC > 0 ? NVC / 2 : 1;
@@ -2191,10 +2192,14 @@ __host__ __device__ constexpr int k2_bf16_kc(int ntc) {
                                                           : ((150 * 1024 / (64 * ntc)) - 8) / 32 * 32;
 }
 
-template <typename T, int NTC, int KC>
-__global__ void __launch_bounds__(64 * k2_waves(NTC))
-k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
-             int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+// GATHER (nullspace mode): the rows are those listed in rowlist (k1s_row_list), *d_rows of them.  A staging slot's
+// row of the chunk after next is looked up one chunk ahead of its load (one list entry per slot and chunk, two
+// register sets), so the gather adds a 4-byte load per slot and no latency to the staging pipeline.
+template <typename T, int NTC, int KC, bool GATHER>
+__device__ __forceinline__ void k2_syrk_body(const T* __restrict__ panel, int64_t rows, int64_t ldp,
+                                             const int2* __restrict__ supers, int ngroups, int ksplit, int nslots,
+                                             int accumulate, double* __restrict__ slab,
+                                             const int* __restrict__ rowlist, const int* __restrict__ d_rows) {
   typedef typename K2Acc<T>::type accT;
   constexpr int K2W = k2_waves(NTC), K2S = k2_slots<T>(NTC);
   constexpr int STRIDE = k2_stride(NTC);
@@ -2203,6 +2208,8 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   __shared__ T lds[2 * BUF];
   int group, ks;
   k2_block_coords(ngroups, group, ks);
+  const int64_t prows = rows;  // GATHER: the panel's rows (the list holds at most these)
+  if constexpr (GATHER) rows = min((int64_t)__builtin_amdgcn_readfirstlane(*d_rows), prows);
   // whole chunks per workgroup: only the panel's last chunk may be partial
   const int64_t nck = (rows + KC - 1) / KC;
   const int64_t r0 = (nck * ks / ksplit) * KC;
@@ -2220,6 +2227,7 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
   constexpr int PER = (KC * NTC * 16 / EP + NT - 1) / NT;  // >= ceil(KC*ldp/EP / NT)
   int loff[PER];
   bool used[PER];
+  int srow[PER], scol[PER];  // GATHER: the slot's row in the chunk and element offset in the row
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int x = threadIdx.x + u * NT;
@@ -2227,7 +2235,15 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
     const int e = EP * x;
     const int row = used[u] ? e / (int)ldp : 0;
     loff[u] = used[u] ? row * STRIDE + (e - row * (int)ldp) : 0;
+    if constexpr (GATHER) {
+      srow[u] = row;
+      scol[u] = used[u] ? e - row * (int)ldp : 0;
+    }
   }
+  auto list_row = [&](int64_t x) -> int64_t {  // a list entry, clamped into the panel
+    const int v = rowlist[x];
+    return v >= 0 && v < prows ? v : 0;
+  };
   uint4 st[PER];
   auto load_chunk = [&](int64_t c0) {
     const uint4* src = reinterpret_cast<const uint4*>(panel + c0 * ldp);
@@ -2235,7 +2251,13 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int x = threadIdx.x + u * NT;
-      st[u] = (used[u] && x < lim) ? src[x] : make_uint4(0u, 0u, 0u, 0u);
+      if constexpr (GATHER) {
+        const bool live = used[u] && c0 + srow[u] < r1;
+        st[u] = live ? *reinterpret_cast<const uint4*>(panel + list_row(c0 + srow[u]) * ldp + scol[u])
+                     : make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        st[u] = (used[u] && x < lim) ? src[x] : make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   };
   auto store_chunk = [&](T* b) {
@@ -2274,6 +2296,19 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 
   const int64_t nfull = (r1 - r0) / KC;
   uint4 sa[PER], sb[PER];  // the two staging register sets (selected at compile time)
+  int64_t la[PER], lb[PER];  // GATHER: the slots' panel rows of the chunk set A / B loads next
+  // GATHER: the list entries of chunk c into set S (clamped like load_full: past the last full chunk, its rows again)
+  auto list_full = [&](int64_t c, auto set) {
+    if constexpr (GATHER) {
+      constexpr int S = decltype(set)::value;
+      const int64_t cc = c < nfull ? c : nfull - 1;
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int64_t v = list_row(r0 + cc * KC + srow[u]);
+        if constexpr (S == 0) la[u] = v; else lb[u] = v;
+      }
+    }
+  };
   auto load_full = [&](int64_t c, auto set) {
     constexpr int S = decltype(set)::value;
     const int64_t cc = c < nfull ? c : nfull - 1;
@@ -2281,8 +2316,13 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
 #pragma unroll
     for (int u = 0; u < PER; ++u) {  // unconditional (an unused slot re-reads the chunk's last 16 bytes)
       const int x = (int)threadIdx.x + u * NT;
-      const uint4 v = src[x < chunk_s ? x : chunk_s - 1];
-      if constexpr (S == 0) sa[u] = v; else sb[u] = v;
+      if constexpr (GATHER) {
+        const uint4 v = *reinterpret_cast<const uint4*>(panel + (S == 0 ? la[u] : lb[u]) * ldp + scol[u]);
+        if constexpr (S == 0) sa[u] = v; else sb[u] = v;
+      } else {
+        const uint4 v = src[x < chunk_s ? x : chunk_s - 1];
+        if constexpr (S == 0) sa[u] = v; else sb[u] = v;
+      }
     }
   };
   auto store_set = [&](auto set, T* b) {
@@ -2332,17 +2372,22 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
     constexpr std::integral_constant<int, 1> B{};
     __syncthreads();  // LDS zeroed
     if (nfull > 0) {
+      if constexpr (GATHER) list_full(0, A);
+      if constexpr (GATHER) list_full(1, B);
       load_full(0, A);
       load_full(1, B);
+      if constexpr (GATHER) list_full(2, A);
       store_set(A, lds);
     }
     __syncthreads();
     int64_t c = 0;
     for (; c + 1 < nfull; c += 2) {  // chunks c (buffer 0, set A) and c + 1 (buffer 1, set B)
+      if constexpr (GATHER) list_full(c + 3, B);
       load_full(c + 2, A);
       mfma_chunk(lds);
       store_set(B, lds + BUF);
       __syncthreads();
+      if constexpr (GATHER) list_full(c + 4, A);
       load_full(c + 3, B);
       mfma_chunk(lds + BUF);
       if (c + 2 < nfull) store_set(A, lds);
@@ -2389,6 +2434,23 @@ k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2*
     SYSID_K2_MASK(12) SYSID_K2_MASK(13) SYSID_K2_MASK(14) SYSID_K2_MASK(15)
 #undef SYSID_K2_MASK
   }
+}
+
+template <typename T, int NTC, int KC>
+__global__ void __launch_bounds__(64 * k2_waves(NTC))
+k2_gram_syrk(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers, int ngroups,
+             int ksplit, int nslots, int accumulate, double* __restrict__ slab) {
+  k2_syrk_body<T, NTC, KC, false>(panel, rows, ldp, supers, ngroups, ksplit, nslots, accumulate, slab, nullptr,
+                                  nullptr);
+}
+// the gathered rows of the nullspace mode (rowlist / d_rows as in k2_gram_syrk_dma)
+template <typename T, int NTC, int KC>
+__global__ void __launch_bounds__(64 * k2_waves(NTC))
+k2_gram_syrk_gather(const T* __restrict__ panel, int64_t rows, int64_t ldp, const int2* __restrict__ supers,
+                    int ngroups, int ksplit, int nslots, int accumulate, double* __restrict__ slab,
+                    const int* __restrict__ rowlist, const int* __restrict__ d_rows) {
+  k2_syrk_body<T, NTC, KC, true>(panel, rows, ldp, supers, ngroups, ksplit, nslots, accumulate, slab, rowlist,
+                                 d_rows);
 }
 
 // ------------------------------------------------------------------------------------------------
