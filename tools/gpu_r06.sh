@@ -41,6 +41,13 @@ for step in "$@"; do
         timeout -k 10 120 python tools/e2e_time.py spot 20000 12 f32 gram >> $OUT/e2e.txt 2>&1 || { echo "e2e failed"; tail $OUT/e2e.txt; exit 1; }
       done
       grep -v amdgpu.ids $OUT/e2e.txt ;;
+    e2eab)
+      bash tools/e2e_ab.sh $TAG/e2eab ${E2E_ROUNDS:-4} "spot 20000 12 f32 gram" $AB_LIBS || exit 1 ;;
+    e2etrace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -f csv -d $OUT/e2etr -o run -- python tools/e2e_time.py spot 20000 4 f32 gram > $OUT/e2etr.log 2>&1 || { echo "e2e trace failed"; tail $OUT/e2etr.log; exit 1; }
+      python tools/trace_timeline.py $(dirname $(find $OUT/e2etr -name "*kernel_trace.csv" | head -1)) 6 30 > $OUT/e2e_timeline.txt; tail -32 $OUT/e2e_timeline.txt
+      SYSID_TRACE_HOST=1 timeout -k 10 120 python tools/e2e_time.py spot 20000 4 f32 gram > $OUT/e2e_host_trace.txt 2>&1 || { echo "host trace failed"; exit 1; }
+      grep -v amdgpu.ids $OUT/e2e_host_trace.txt | tail -8 ;;
     *)
       echo "unknown step $step"; exit 1 ;;
   esac
