@@ -246,6 +246,9 @@ int32_t sysid_debug_layout(const sysid_engine* e, int32_t* offsets12);
 int32_t sysid_debug_k1_config(const sysid_engine* e, int32_t* cfg4);
 /* K2 Gram deal chosen at model creation: {tile columns, tile slots of the f64, f32 and bf16 deals}. */
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4);
+/* Tests: the host entry points stage their inputs in `chunks` equal chunks (1..64; 0 restores the default: a first
+ * chunk of ~30% of N, then the rest) — exercises the multi-chunk staging pipeline. */
+int32_t sysid_debug_set_stage_chunks(sysid_engine* e, int32_t chunks);
 
 /* Same helper run on the device: lane l (0..63) computes column l % 10 into fw_64x6[l*6 .. l*6+5]. */
 int32_t sysid_debug_body_column_device(const double* body24, double* fw_64x6);

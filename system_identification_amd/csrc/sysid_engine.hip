@@ -158,6 +158,7 @@ struct sysid_engine {
   double* d_out = nullptr;   // host API: de-interleaved stacked outputs (grow-only)
   size_t out_cap = 0;
   int host_register = -1;    // host API copies: 1 page-lock the caller's arrays, 0 pageable, -1 by size
+  int stage_chunks = 0;      // host API staging: k > 0 forces k equal staged chunks (sysid_debug_set_stage_chunks)
   double* d_dump = nullptr;  // diagnostics only
   double* h_stage = nullptr;  // host API: page-locked staging of the inputs' wire blocks (grow-only)
   size_t h_stage_cap = 0;
@@ -166,9 +167,6 @@ struct sysid_engine {
   double* h_gram = nullptr;   // host API: page-locked copy of the (W+1)^2 Gram, one DMA back (grow-only)
   HostPool* pool = nullptr;   // host API: packing threads (stage_inputs), started on first use
   hipStream_t copy_stream = nullptr;     // host API: the staged input chunks' DMA (created on first use)
-  static constexpr int MAX_COPY = 4;
-  hipStream_t copy_more[MAX_COPY] = {};  // further copy streams (SYSID_COPY_STREAMS > 1): chunk c on stream c % n
-  int ncopy = 1;
   std::vector<hipEvent_t> stage_ev;      // host API: one event per staged chunk (grow-only)
   std::string err;
 };
@@ -611,16 +609,7 @@ int warm_copy_stream(sysid_engine* e, hipStream_t* sp) {
 }
 int ensure_copy_stream(sysid_engine* e) {
   if (e->copy_stream) return SYSID_OK;
-  if (int rc = warm_copy_stream(e, &e->copy_stream)) return rc;
-  // SYSID_COPY_STREAMS=n (dev knob): the staged chunks' DMAs round-robin over n copy streams
-  if (const char* v = std::getenv("SYSID_COPY_STREAMS")) e->ncopy = std::max(1, std::min(e->MAX_COPY, std::atoi(v)));
-  for (int k = 1; k < e->ncopy; ++k)
-    if (int rc = warm_copy_stream(e, &e->copy_more[k])) return rc;
-  return SYSID_OK;
-}
-hipStream_t copy_stream_of(const sysid_engine* e, int c) {
-  const int k = c % e->ncopy;
-  return k == 0 ? e->copy_stream : e->copy_more[k];
+  return warm_copy_stream(e, &e->copy_stream);
 }
 
 // Wire format of the host entry points' inputs (K0W, sysid_kernels.h): per staged chunk of n samples, the q rows in
@@ -665,12 +654,12 @@ class Stager {
   int begin(const HostInputs& in, const std::vector<int64_t>* bounds = nullptr) {
     sysid_engine* e = e_;
     in_ = in;
-    int parts = 2;  // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few
-                    // (Spot 20k Gram-only e2e, 1 / 2 / 4 / 8 chunks: 0.74 / 0.67 / 0.75 / 1.05 ms; profiles/r04_h)
-    if (const char* v = std::getenv("SYSID_STAGE_CHUNKS")) parts = std::max(1, std::min(64, std::atoi(v)));
+    // chunks: the first one's pack + DMA is the pipeline's fill, the kernels' efficiency wants few (Spot 20k
+    // Gram-only e2e, 1 / 2 / 4 / 8 chunks: 0.74 / 0.67 / 0.75 / 1.05 ms; profiles/r04_h)
+    const int parts = e->stage_chunks > 0 ? e->stage_chunks : 2;
     const int64_t CH = std::max<int64_t>(2048, (N_ + parts - 1) / parts);
     b_.clear();
-    if (bounds && !std::getenv("SYSID_STAGE_CHUNKS")) {
+    if (bounds && e->stage_chunks == 0) {
       b_ = *bounds;
     } else {
       for (int64_t c0 = 0; c0 < N_; c0 += CH) b_.push_back(c0);
@@ -758,7 +747,7 @@ class Stager {
     const int64_t c0 = b_[c], n = b_[c + 1] - c0;
     const Wire w = wire_layout(e->nq, nd_, e->nc, n, in_.qsz);
     const unsigned char* hs = reinterpret_cast<const unsigned char*>(e->h_stage) + off_[c];
-    hipStream_t cs = copy_stream_of(e, c);
+    hipStream_t cs = e->copy_stream;
     if (hipMemcpyAsync(e->d_wire + off_[c], hs, (size_t)w.bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
         hipEventRecord(e->stage_ev[c], cs) != hipSuccess ||
         hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
@@ -1139,7 +1128,6 @@ int32_t sysid_model_create(const void* packed, size_t nbytes, int32_t device, sy
   if (st == hipSuccess) st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (st == hipSuccess) st = hipMalloc(&e->d_mimg, img.size() * sizeof(uint32_t));
   if (st == hipSuccess) st = hipMemcpy(e->d_mimg, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-  if (const char* v = std::getenv("SYSID_HOST_REGISTER")) e->host_register = std::atoi(v) != 0 ? 1 : 0;
   if (st == hipSuccess) st = hipMalloc(&e->d_work, WORK_BYTES);
   if (st == hipSuccess) st = hipMemset(e->d_work, 0, WORK_BYTES);
   for (int p = 0; p < 3; ++p) {
@@ -1228,8 +1216,6 @@ void sysid_destroy(sysid_engine* e) {
   delete e->pool;
   for (hipEvent_t x : e->stage_ev) (void)hipEventDestroy(x);
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
-  for (hipStream_t x : e->copy_more)
-    if (x) (void)hipStreamDestroy(x);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1534,25 +1520,18 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
                          ((flags & SYSID_EMIT_FRICTION) && (B_v || B_c) && e->nj);
   const bool gram_only = want_gram && !panel_out;
   const int gp = gram_prec(flags);
-  // Gram-only staged chunks (SYSID_STAGE_CHUNKS=k: k equal chunks instead).  Two staged chunks: a short first one,
+  // Gram-only staged chunks.  Two staged chunks: a short first one,
   // whose DMA lands early so the kernels start while the second chunk's DMA runs, then the rest (against three or more
   // chunks, which each add a K1 tail, a row list and a K2 pass to the kernel chain: profiles/r05_s4).  The first chunk
   // is ~30% of N in half K1 rounds (a round = every resident wave one step), at least one round: Spot 20k Gram-only
   // e2e, float32 q, 5 interleaved rounds of 12 calls: first chunk 4,096 / 5,120 / 6,144 / 7,168 samples, median
-  // 0.556 / 0.530 / 0.526 / 0.532 ms, best 0.530 / 0.514 / 0.499 / 0.509 (profiles/r05_s24).
-  // SYSID_STAGE_SPLIT=3: a one-round chunk, then two chunks of whole rounds.
+  // 0.556 / 0.530 / 0.526 / 0.532 ms, best 0.530 / 0.514 / 0.499 / 0.509 (profiles/r05_s24).  The round-5 sweeps of
+  // these bounds, of more chunks and of more copy streams ran on environment knobs that round 6 removed (git history).
   std::vector<int64_t> round_bounds;
   const bool big = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20);
   if (gram_only && big) {
-    static const int split = [] {
-      const char* v = std::getenv("SYSID_STAGE_SPLIT");
-      return v && std::atoi(v) == 3 ? 3 : 2;
-    }();
     const int64_t R = k1_round_samples(e, gp, gram_nullspace(e, flags));
-    if (R > 0 && N >= 3 * R && split == 3) {
-      const int64_t mid = R + ((N - R + 2 * R - 1) / (2 * R)) * R;  // whole rounds, the larger half first
-      round_bounds = {0, R, std::min(mid, N - 1), N};
-    } else if (R > 0 && N >= 2 * R) {
+    if (R > 0 && N >= 2 * R) {
       const int64_t half = std::max<int64_t>(1, R / 2);
       const int64_t first = std::min(std::max((3 * N / 10 + half - 1) / half * half, R), N - R);
       round_bounds = {0, first, N};
@@ -1562,18 +1541,6 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
   } else {
     round_bounds = {0, N};  // one chunk (stacked outputs read every sample in one K1; small inputs)
     if (big && !gram_only) round_bounds.clear();  // stacked outputs, large: the Stager's default chunks
-  }
-  if (const char* v = std::getenv("SYSID_STAGE_BOUNDS")) {  // dev knob: explicit inner chunk bounds "b1,b2,..."
-    if (gram_only && big) {
-      round_bounds = {0};
-      for (const char* p = v; *p;) {
-        const long long b = std::strtoll(p, const_cast<char**>(&p), 10);
-        if (b > round_bounds.back() && b < N) round_bounds.push_back(b);
-        while (*p == ',' || *p == ' ') ++p;
-        if (*p && (*p < '0' || *p > '9')) break;
-      }
-      round_bounds.push_back(N);
-    }
   }
   int rc;
   if ((rc = grow(e, reinterpret_cast<void**>(&e->d_in), &e->in_cap, (size_t)e->in_rows * N * sizeof(double))))
@@ -1591,8 +1558,6 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
   auto fail = [&](int code) {
     (void)hipStreamSynchronize(st);
     if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
-    for (hipStream_t x : e->copy_more)
-      if (x) (void)hipStreamSynchronize(x);
     host_unregister(e, reg);
     stager.finish();
     return code == SYSID_E_CONTACT && stager.contacts_bad() ? contact_error() : code;
@@ -1823,6 +1788,12 @@ int32_t sysid_internal_xchg_unpack(const sysid_engine* e, const double* d_x, dou
   hipLaunchKernelGGL(xchg_unpack, dim3((unsigned)(((int64_t)n * n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), d_x, n, d_gram);
   return hipGetLastError() == hipSuccess ? SYSID_OK : SYSID_E_DEVICE;
+}
+
+int32_t sysid_debug_set_stage_chunks(sysid_engine* e, int32_t chunks) {
+  if (!e || chunks < 0 || chunks > 64) return set_err(e, SYSID_E_INVALID, "stage chunks %d outside 0..64", chunks);
+  e->stage_chunks = chunks;
+  return SYSID_OK;
 }
 
 int32_t sysid_debug_k2_config(const sysid_engine* e, int32_t* cfg4) {

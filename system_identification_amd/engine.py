@@ -61,6 +61,7 @@ SIGNATURES = [
     ("sysid_gram_rows", _c.c_int32, [_vp, _c.c_uint32]),
     ("sysid_set_gram_chunk_bytes", _c.c_int32, [_vp, _c.c_uint64]),
     ("sysid_debug_k2_config", _c.c_int32, [_vp, _c.POINTER(_c.c_int32)]),
+    ("sysid_debug_set_stage_chunks", _c.c_int32, [_vp, _c.c_int32]),
     ("sysid_time_stages", _c.c_int32, [_vp, _vp, _c.c_int64, _c.c_int64, _c.c_uint32, _vp, _c.c_int64, _vp,
                                        _vp, _c.c_size_t, _c.c_int32, _dp]),
     ("sysid_gram_workspace_bytes", _c.c_size_t, [_vp, _c.c_int64]),
@@ -387,6 +388,10 @@ class Engine:
             ctypes.c_void_p(bufs["gram"].data_ptr()), ctypes.c_void_p(bufs["ws"].data_ptr()),
             int(bufs["ws"].numel()), ctypes.c_void_p(st))
         self._check(rc)
+
+    def set_stage_chunks(self, chunks: int) -> None:
+        """Tests: stage the host entry points' inputs in `chunks` equal chunks (0 = the default bounds)."""
+        self._check(self.lib.sysid_debug_set_stage_chunks(self._h, int(chunks)))
 
     def set_gram_chunk_bytes(self, nbytes: int) -> None:
         """Chunk panel size of the Gram-only path (>= 1 MiB; 0 = the 4 GiB default).  alloc_gram_device /

@@ -355,19 +355,16 @@ def test_gram_only_chunked(robot, N):
                                                     ("spot", 20001, 0, 0), ("spot", 10000, 0, 0),
                                                     ("spot", 40000, 0, 64 << 20),
                                                     ("g1_29dof", 9001, 0, 0)])
-def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk, monkeypatch):
+def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk):
     """Host Gram-only entry point with its inputs staged in `chunks` wire blocks (each chunk packed as its own block,
     sent as one DMA and widened by K0W into the row-major block its K1 reads), ragged last chunk, and staged chunks
     larger than the workspace's panel chunk (ws_chunk bytes: several K1 launches per staged block): the same normal
     equations as the device entry point on the row-major block, to rounding.  chunks = 0: the default bounds (a
     first chunk of one K1 round, then two chunks of whole rounds)."""
     import torch
-    if chunks:
-        monkeypatch.setenv("SYSID_STAGE_CHUNKS", str(chunks))
-    else:
-        monkeypatch.delenv("SYSID_STAGE_CHUNKS", raising=False)
     model = load_robot(robot)
     e = Engine(model)
+    e.set_stage_chunks(chunks)
     if ws_chunk:
         e.set_gram_chunk_bytes(ws_chunk)
     d = generate(model, N, config_index=4)
