@@ -84,6 +84,13 @@ constexpr int BODY_STRIDE = 26;
 //     in registers until every entry has been computed (K1_POV_BUF passes at most).  G1: 2,916 -> 2,452
 //     doubles per sample, so one workgroup of 8 one-sample waves fits a CU's 160 KB (was 3 x 2 waves).
 constexpr int K1_POV_BUF = 12;  // P passes (of 64 entries) a P overlay may hold in registers
+// The bf16 Q-form's f32 row operands, by row pairs (rows 2p, 2p + 1 at 28 p floats): Q entries interleaved
+// (2 j + (r & 1): Q_j of row r, zero past the sample's rows), then the motion axes as [J_r[0], J_r[1], J_r1[0], J_r1[1],
+// J_r[3], J_r[4], J_r1[3], J_r1[4], J_r[2], J_r1[2], J_r[5], J_r1[5]] (r1 = r + 1), so a lane's operands of a pair are a
+// few aligned 16- and 8-byte reads already in packed-FMA order.  One pair past the last is readable (the row loop's
+// operand prefetch).
+__host__ __device__ constexpr int k1q32_pairs(int nv) { return (nv + 1) / 2 + 1; }
+__host__ __device__ constexpr int k1q32_doubles(int nv) { return k1q32_pairs(nv) * 14; }
 struct WLay {
   int in, body, W, Pt, Jw, pf, Jc, M, P, H1, tp, dqs, Z, q32, total;
 };
@@ -124,7 +131,7 @@ __host__ __device__ inline WLay wave_layout(int in_rows, int nv, int NJ, int nc,
     l.H1 = D;                   // unused
     // f32 copies of every row's Q entries (8, zero past k) and motion axis (6) for the bf16 row loop: converted
     // once per sample instead of by every lane on every row
-    l.q32 = take(nv * 7);
+    l.q32 = take(k1q32_doubles(nv));
     l.total = o;
     return l;
   }
@@ -1640,9 +1647,24 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
       const int nyh = 2 * nbody;  // even: both lanes of a pair are always active together
       if constexpr (std::is_same_v<OutT, __bf16>) {
         float* q32w = reinterpret_cast<float*>(wr + L.q32);
-        for (int e2 = hl; e2 < nv * 14; e2 += HW) {
-          const int r = e2 / 14, c = e2 - 14 * r;
-          q32w[e2] = c < 8 ? (c < K1_QF_KMAX ? (float)Qt[r * K1_QF_KMAX + c] : 0.0f) : (float)Jws[6 * r + c - 8];
+        for (int e2 = hl; e2 < k1q32_pairs(nv) * 28; e2 += HW) {
+          const int pr = e2 / 28, x = e2 - 28 * pr;
+          int row, c;
+          if (x < 16) {
+            row = 2 * pr + (x & 1);
+            c = x >> 1;
+          } else if (x < 24) {
+            const int y = x - 16;
+            row = 2 * pr + ((y >> 1) & 1);
+            c = 3 * (y >> 2) + (y & 1);
+          } else {
+            const int y = x - 24;
+            row = 2 * pr + (y & 1);
+            c = 2 + 3 * (y >> 1);
+          }
+          float v = 0.0f;
+          if (row < nv) v = x < 16 ? (c < K1_QF_KMAX ? (float)Qt[row * K1_QF_KMAX + c] : 0.0f) : (float)Jws[6 * row + c];
+          q32w[e2] = v;
         }
         wsync();
       }
@@ -1703,47 +1725,44 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
           // instruction at the cost of one f64 FMA); G and the block's outputs carry
           // ~1e-7 relative error, far below the bf16 rounding (2^-9) the panel gets anyway; K and F6 are formed in
           // f64 and rounded once.
-          const float* q32 = reinterpret_cast<const float*>(wr + L.q32);  // [r][Q 0..7 | J 0..5]
+          const float* q32 = reinterpret_cast<const float*>(wr + L.q32);  // row pairs (k1q32_pairs)
+          // Rows in pairs: the pair's two third components of G share packed FMAs, and the loop body takes two pairs
+          // with two operand sets (pair p + 1's LDS reads in flight while pair p is multiplied, no register copies
+          // between iterations).  Stores: the wave-uniform row base (one sample per wave) plus this lane's 32-bit byte
+          // offset (no 64-bit address per row).
+          const uint32_t sb0 = (uint32_t)((10 * (i - 1) + 4 * h) * (int)sizeof(OutT));
+          const uint32_t sb2 = sb0 + (uint32_t)((h ? 4 : 2) * (int)sizeof(OutT));
+          char* obase = reinterpret_cast<char*>(out);
           auto rows_f32 = [&](auto kqc) {
             constexpr int KQ = decltype(kqc)::value;
-            f32x2_t K01[KQ];
-            float K2[KQ];
+            f32x2_t K01[KQ], K22[KQ];
 #pragma unroll
             for (int j = 0; j < KQ; ++j) {
               K01[j] = f32x2_t{(float)Kq[j][0], (float)Kq[j][1]};
-              K2[j] = (float)Kq[j][2];
+              const float k2 = (float)Kq[j][2];
+              K22[j] = f32x2_t{k2, k2};
             }
             f32x2_t Fp[3][6];  // Fp[p][q] = (F6[2p][q], F6[2p + 1][q])
 #pragma unroll
             for (int pp = 0; pp < 3; ++pp)
 #pragma unroll
               for (int q = 0; q < 6; ++q) Fp[pp][q] = f32x2_t{(float)F6[2 * pp][q], (float)F6[2 * pp + 1][q]};
-            float qn[K1_QF_KMAX], jn[3];
-            auto row_ld = [&](int r, float* qv, float* jv) {
-              const float* qrow = q32 + 14 * r;
-#pragma unroll
-              for (int j = 0; j < K1_QF_KMAX; ++j) qv[j] = qrow[j];
-#pragma unroll
-              for (int c = 0; c < 3; ++c) jv[c] = qrow[8 + c3 + c];
+            // a pair's operands (k1q32_pairs layout): qp[j] = (Q_j of row r, of row r + 1), jq = (J_r[c3], J_r[c3 + 1],
+            // J_r1[c3], J_r1[c3 + 1]), j2 = (J_r[c3 + 2], J_r1[c3 + 2])
+            struct PairOps {
+              f32x2_t qp[KQ];
+              flt4 jq;
+              f32x2_t j2;
             };
-            row_ld(0, qn, jn);
-#pragma unroll 1
-            for (int r = 0; r < nrows; ++r) {
-              const float sf = ((smask >> r) & 1ull) ? 1.0f : 0.0f;
-              float qr[K1_QF_KMAX], jr[3];
+            auto pair_ld = [&](int pr, PairOps& o) {
+              const float* b = q32 + 28 * pr;
 #pragma unroll
-              for (int j = 0; j < K1_QF_KMAX; ++j) qr[j] = qn[j];
-#pragma unroll
-              for (int c = 0; c < 3; ++c) jr[c] = jn[c];
-              row_ld(r + 1 < nrows ? r + 1 : r, qn, jn);
-              f32x2_t g01 = f32x2_t{sf * jr[0], sf * jr[1]};
-              float g2 = sf * jr[2];
-#pragma unroll
-              for (int j = 0; j < KQ; ++j) {
-                g01 -= qr[j] * K01[j];
-                g2 -= qr[j] * K2[j];
-              }
-              const float G[6] = {g01.x, g01.y, g2, pair_swap_f32(g01.x), pair_swap_f32(g01.y), pair_swap_f32(g2)};
+              for (int j = 0; j < KQ; ++j) o.qp[j] = *reinterpret_cast<const f32x2_t*>(b + 2 * j);
+              o.jq = *reinterpret_cast<const flt4*>(b + 16 + 4 * h);
+              o.j2 = *reinterpret_cast<const f32x2_t*>(b + 24 + 2 * h);
+            };
+            auto emit = [&](int r, float g0, float g1, float g2) {
+              const float G[6] = {g0, g1, g2, pair_swap_f32(g0), pair_swap_f32(g1), pair_swap_f32(g2)};
               f32x2_t y01 = f32x2_t{0.0f, 0.0f}, y23 = y01, y45 = y01;
 #pragma unroll
               for (int q = 0; q < 6; ++q) {
@@ -1753,10 +1772,41 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
               // outputs 4, 5: h = 1 lanes only, whose slots 3..5 are zero
 #pragma unroll
               for (int q = 0; q < 3; ++q) y45 += G[q] * Fp[2][q];
-              __bf16* o2 = reinterpret_cast<__bf16*>(oi + (int64_t)r * ldp);
-              panel_store_f32(o2, y01.x, y01.y);
-              panel_store_f32(o2 + 2, y23.x, y23.y);
-              panel_store_f32(o2 + (h ? 4 : 2), h ? y45.x : y23.x, h ? y45.y : y23.y);
+              char* rb = obase + (int64_t)r * ldp * (int64_t)sizeof(OutT);  // wave-uniform
+              uint32_t o0 = sb0, o2 = sb2;
+              asm volatile("" : "+v"(o0), "+v"(o2));
+              panel_store_f32(reinterpret_cast<__bf16*>(rb + o0), y01.x, y01.y);
+              panel_store_f32(reinterpret_cast<__bf16*>(rb + o0 + 2 * sizeof(OutT)), y23.x, y23.y);
+              panel_store_f32(reinterpret_cast<__bf16*>(rb + o2), h ? y45.x : y23.x, h ? y45.y : y23.y);
+            };
+            auto pair_do = [&](int r, const PairOps& o) {  // rows r (even) and r + 1 (< nrows only)
+              const unsigned long long sm = smask >> r;
+              const f32x2_t sf = f32x2_t{(sm & 1ull) ? 1.0f : 0.0f, (sm & 2ull) ? 1.0f : 0.0f};
+              f32x2_t ga = sf.x * f32x2_t{o.jq.x, o.jq.y}, gb = sf.y * f32x2_t{o.jq.z, o.jq.w};
+              f32x2_t g2 = sf * o.j2;
+#pragma unroll
+              for (int j = 0; j < KQ; ++j) {
+                ga -= o.qp[j].x * K01[j];
+                gb -= o.qp[j].y * K01[j];
+                g2 -= o.qp[j] * K22[j];
+              }
+              emit(r, ga.x, ga.y, g2.x);
+              if (r + 1 < nrows) emit(r + 1, gb.x, gb.y, g2.y);
+            };
+            PairOps A, B;  // two operand sets: pair p + 1's reads are in flight while pair p is multiplied
+            pair_ld(0, A);
+            int r = 0;
+#pragma unroll 1
+            for (; r + 4 <= nrows; r += 4) {
+              pair_ld((r >> 1) + 1, B);
+              pair_do(r, A);
+              pair_ld((r >> 1) + 2, A);
+              pair_do(r + 2, B);
+            }
+            if (r < nrows) {  // 1..3 rows left, rows r, r + 1 in set A
+              pair_ld((r >> 1) + 1, B);
+              pair_do(r, A);
+              if (r + 2 < nrows) pair_do(r + 2, B);
             }
           };
           if (kq <= 3) rows_f32(std::integral_constant<int, 3>{});
@@ -1909,9 +1959,9 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
             const f32x2_t sc2 = f32x2_t{fcol[0] ? (float)sc[0] : 0.0f, fcol[1] ? (float)sc[1] : 0.0f};
             for (int r = fg; r < nrows; r += NG, po += pstep) {
               f32x2_t pe = f32x2_t{r == bd + jc[0] ? 1.0f : 0.0f, r == bd + jc[1] ? 1.0f : 0.0f};
-              const float* qrow = q32 + 14 * r;
+              const float* qrow = q32 + 28 * (r >> 1) + (r & 1);  // k1q32_pairs layout: Q_j at 2 j
 #pragma unroll
-              for (int j = 0; j < K1_QF_KMAX; ++j) pe -= qrow[j] * qc2[j];
+              for (int j = 0; j < K1_QF_KMAX; ++j) pe -= qrow[2 * j] * qc2[j];
               const float t = (float)tps[r];
               pe *= sc2;
               panel_store_f32(reinterpret_cast<__bf16*>(po), tcol[0] ? t : pe.x, tcol[1] ? t : pe.y);
