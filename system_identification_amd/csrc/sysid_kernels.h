@@ -1957,14 +1957,33 @@ __device__ __forceinline__ void k1_body(const K1Params& kp, const uint32_t* __re
 #pragma unroll
             for (int j = 0; j < K1_QF_KMAX; ++j) qc2[j] = f32x2_t{(float)qc[j][0], (float)qc[j][1]};
             const f32x2_t sc2 = f32x2_t{fcol[0] ? (float)sc[0] : 0.0f, fcol[1] ? (float)sc[1] : 0.0f};
-            for (int r = fg; r < nrows; r += NG, po += pstep) {
-              f32x2_t pe = f32x2_t{r == bd + jc[0] ? 1.0f : 0.0f, r == bd + jc[1] ? 1.0f : 0.0f};
-              const float* qrow = q32 + 28 * (r >> 1) + (r & 1);  // k1q32_pairs layout: Q_j at 2 j
+            // row pairs (the k1q32_pairs layout: a pair's Q entries in three 16-byte reads), group fg taking every NG-th
+            // pair; stores from the sample's wave-uniform base (one sample per wave) plus the lane's 32-bit offset
+            char* fbase = reinterpret_cast<char*>(out);
+            const uint32_t frow = (uint32_t)ldp * (uint32_t)sizeof(OutT), fstep = 2 * (uint32_t)NG * frow;
+            uint32_t fo = (uint32_t)((2 * fg * (int)ldp + kp.wy + 2 * m) * (int)sizeof(OutT));  // pair fg's first row
+            const int npr = (nrows + 1) >> 1;
+            for (int pr = fg; pr < npr; pr += NG, fo += fstep) {
+              const float* b = q32 + 28 * pr;
+              f32x2_t qp[K1_QF_KMAX];
 #pragma unroll
-              for (int j = 0; j < K1_QF_KMAX; ++j) pe -= qrow[2 * j] * qc2[j];
-              const float t = (float)tps[r];
-              pe *= sc2;
-              panel_store_f32(reinterpret_cast<__bf16*>(po), tcol[0] ? t : pe.x, tcol[1] ? t : pe.y);
+              for (int j = 0; j < K1_QF_KMAX; ++j) qp[j] = *reinterpret_cast<const f32x2_t*>(b + 2 * j);
+              const int r0 = 2 * pr, r1 = r0 + 1;
+              f32x2_t pa = f32x2_t{r0 == bd + jc[0] ? 1.0f : 0.0f, r0 == bd + jc[1] ? 1.0f : 0.0f};
+              f32x2_t pb = f32x2_t{r1 == bd + jc[0] ? 1.0f : 0.0f, r1 == bd + jc[1] ? 1.0f : 0.0f};
+#pragma unroll
+              for (int j = 0; j < K1_QF_KMAX; ++j) {
+                pa -= qp[j].x * qc2[j];
+                pb -= qp[j].y * qc2[j];
+              }
+              pa *= sc2;
+              pb *= sc2;
+              asm volatile("" : "+v"(pb));  // formed beside pa (interleaved packed FMAs), not sunk into the odd-row branch
+              const float ta = (float)tps[r0], tb = (float)tps[r1 < nrows ? r1 : r0];
+              uint32_t o = fo, o1 = fo + frow;
+              asm volatile("" : "+v"(o), "+v"(o1));
+              panel_store_f32(reinterpret_cast<__bf16*>(fbase + o), tcol[0] ? ta : pa.x, tcol[1] ? ta : pa.y);
+              if (r1 < nrows) panel_store_f32(reinterpret_cast<__bf16*>(fbase + o1), tcol[0] ? tb : pb.x, tcol[1] ? tb : pb.y);
             }
           } else {
           double qn[K1_QF_KMAX], tn = 0.0;  // row r + NG's Q entries and torque, read while row r is formed

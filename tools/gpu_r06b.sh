@@ -14,6 +14,13 @@ for step in "$@"; do
       timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "spot or solo or quad or golden or determin" > $OUT/pytest_quick.log 2>&1; rc=$?
       echo "quick rc $rc"; grep -E " passed| failed" $OUT/pytest_quick.log | tail -2; grep -E "FAILED|Error" $OUT/pytest_quick.log | head
       [ $rc -eq 0 ] || exit 1 ;;
+    libtest)  # the parity subset that caught the round's friction-store failure, on each $TEST_LIBS build
+      for lib in $TEST_LIBS; do
+        n=$(basename $lib .so)
+        SYSID_LIB=$PWD/$lib timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "whole_panel or two_streams or determinism or config4_shard" > $OUT/libtest_$n.log 2>&1; rc=$?
+        echo "libtest $n rc $rc: $(grep -E ' passed| failed' $OUT/libtest_$n.log | tail -1)"
+        [ $rc -eq 0 ] || exit 1  # any failure (a fault reads as a failed test too) ends the session
+      done ;;
     pmc)
       bash tools/pmc_ab.sh $OUT/pmc ${PMC_ROBOT:-spot} $PMC_LIBS || exit 1 ;;
     *)
