@@ -527,8 +527,10 @@ int launch_gram_chunked(sysid_engine* e, const double* d_in, int64_t N, int64_t 
       if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 1, rcount, zeroed)))
         return rc;
       const unsigned nseg = (unsigned)((n + (1 << K1_SEG_LOG) - 1) >> K1_SEG_LOG);
-      hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
-      hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, rseg, (int)n, e->nv, rowlist, d_rows);
+      const bool onepass = nseg <= (unsigned)K1S_ONEPASS_SEGS;
+      if (!onepass) hipLaunchKernelGGL(k1s_seg_sums, dim3(nseg), dim3(256), 0, st, rcount, (int)n, rseg);
+      hipLaunchKernelGGL(k1s_row_list, dim3(nseg), dim3(256), 0, st, rcount, onepass ? nullptr : rseg, (int)n, e->nv,
+                         rowlist, d_rows);
       HIP_TRY(e, hipGetLastError());
     } else if ((rc = launch_k1(e, cin, n, cld, panel, ldc, work, st, nullptr, 0, prec, 0, nullptr, zeroed))) {
       return rc;
@@ -641,6 +643,10 @@ struct HostInputs {
   int64_t ld;
 };
 
+#ifndef SYSID_ZC_FIRST  // 1: the first staged chunk is widened straight from the staging block (no DMA); -D for A/B
+#define SYSID_ZC_FIRST 1
+#endif
+
 class Stager {
  public:
   Stager(sysid_engine* e, int64_t N) : e_(e), N_(N) {}
@@ -650,7 +656,10 @@ class Stager {
   // Host threads (the engine's pool) pack chunk after chunk of the caller's rows into the engine's page-locked
   // staging block in the wire format; stage(c) waits until chunk c is packed, sends it as ONE DMA on the engine's
   // copy stream into the device wire buffer, makes `st` wait for that DMA and widens the chunk into the row-major
-  // float64 input block e->d_in (ld = N) with K0W, which also zeroes K1's claim counters (`work`).
+  // float64 input block e->d_in (ld = N) with K0W, which also zeroes K1's claim counters (`work`).  Chunk 0 has no
+  // DMA: K0W reads it from the mapped staging block over PCIe, which takes the copy engine's time (~55-65 us for
+  // Spot's 6,144-sample first chunk) without the copy-engine -> compute-stream hand-off after it (~17 us);
+  // Spot 20k Gram-only e2e 0.507 -> 0.488 ms (median of per-run best, profiles/r06_s16).
   int begin(const HostInputs& in, const std::vector<int64_t>* bounds = nullptr) {
     sysid_engine* e = e_;
     in_ = in;
@@ -747,14 +756,24 @@ class Stager {
     const int64_t c0 = b_[c], n = b_[c + 1] - c0;
     const Wire w = wire_layout(e->nq, nd_, e->nc, n, in_.qsz);
     const unsigned char* hs = reinterpret_cast<const unsigned char*>(e->h_stage) + off_[c];
-    hipStream_t cs = e->copy_stream;
-    if (hipMemcpyAsync(e->d_wire + off_[c], hs, (size_t)w.bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipEventRecord(e->stage_ev[c], cs) != hipSuccess ||
-        hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
-      return set_err(e, SYSID_E_DEVICE, "input copy failed");
+    const unsigned char* src = e->d_wire + off_[c];
+    if (c == 0 && SYSID_ZC_FIRST) {
+      // chunk 0, the pipeline's fill: K0W reads the page-locked staging block over PCIe itself, so the compute
+      // stream starts on it without a copy-engine -> compute hand-off
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, e->h_stage, 0) != hipSuccess)
+        return set_err(e, SYSID_E_DEVICE, "staging block not mapped");
+      src = static_cast<const unsigned char*>(dp) + off_[c];
+    } else {
+      hipStream_t cs = e->copy_stream;
+      if (hipMemcpyAsync(e->d_wire + off_[c], hs, (size_t)w.bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
+          hipEventRecord(e->stage_ev[c], cs) != hipSuccess ||
+          hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
+        return set_err(e, SYSID_E_DEVICE, "input copy failed");
+    }
     const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (n + 1023) / 1024));
-    hipLaunchKernelGGL(k0_widen, dim3(gx, (unsigned)(e->nq + nd_ + e->nc)), dim3(256), 0, st, e->d_wire + off_[c], n,
-                       e->nq, nd_, in_.qsz, w.d, w.c, e->d_in + c0, N_, work, (int)(WORK_BYTES / 8));
+    hipLaunchKernelGGL(k0_widen, dim3(gx, (unsigned)(e->nq + nd_ + e->nc)), dim3(256), 0, st, src, n, e->nq, nd_,
+                       in_.qsz, w.d, w.c, e->d_in + c0, N_, work, (int)(WORK_BYTES / 8));
     HIP_TRY(e, hipGetLastError());
     stamp();  // chunk c's DMA and widening enqueued
     return SYSID_OK;

@@ -506,6 +506,7 @@ __host__ __device__ inline void block_column(const double* F, int p, double* fw)
 // [s·nv, s·nv + m) of the chunk panel and records m in rcount[s], from which k1s_seg_sums / k1s_row_list build
 // the list of live rows the Gram kernels gather.
 constexpr int K1_SEG_LOG = 10;  // samples per row-count segment of the CMP mode (1024)
+constexpr int K1S_ONEPASS_SEGS = 32;  // up to this many segments k1s_row_list sums the earlier counts itself
 constexpr int K1_CMP_KMAX = 12;
   // CMP mode: at most 12 contact rows (4 contact frames; the host checks)
 // QF: the Q-form of the runtime-nv kernel for at most K1_QF_KMAX contact rows (G1: 6): P = I - QᵀQ is never
@@ -2086,8 +2087,9 @@ k1_regressor_panel(const K1Params kp, const uint32_t* __restrict__ mimg_g, const
 // ------------------------------------------------------------------------------------------------
 // K1s (nullspace mode): the list of live chunk-panel rows, in sample order, for the Gram kernels to gather.
 // k1s_seg_sums: rseg[b] = the rows of the 1024 samples of segment b.  k1s_row_list: block b's first list
-// position is the sum of the earlier segments' rows, then a block scan of its own samples' counts; sample s
-// with m rows lists s·nv, ..., s·nv + m - 1.  The last block writes the total.  Plain stores and integer
+// position is the sum of the earlier segments' rows (from rseg, or, rseg = nullptr, summed from rcount itself: one
+// launch instead of two for chunks of at most K1S_ONEPASS_SEGS segments), then a block scan of its own samples'
+// counts; sample s with m rows lists s·nv, ..., s·nv + m - 1.  The last block writes the total.  Plain stores and integer
 // arithmetic only (no atomics, nothing to zero beforehand): deterministic, and graph replays start clean.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int k1s_wave_incl(int v, int lane) {  // inclusive scan over the 64 lanes
@@ -2111,7 +2113,8 @@ __global__ void __launch_bounds__(256) k0_zero_u64(unsigned long long* __restric
 // Host entry points' wire format (sysid_engine.hip, wire_layout): one block per staged chunk of n samples — q rows
 // (nq x n, float32 when the caller's q is float32 as read_data returns it, else float64), the dq / ddq / tau rows
 // (nd x n float64) and the contact rows (nc x n bytes: 1 where the value is non-zero, the only property the
-// projector reads) — sent as one DMA.  K0W widens chunk [c0, c0 + n) into the row-major float64 input block K1
+// projector reads) — sent as one DMA (the first chunk: read by K0W from the mapped page-locked staging block
+// itself, sysid_engine.hip Stager::stage).  K0W widens chunk [c0, c0 + n) into the row-major float64 input block K1
 // reads (rows x ld) and zeroes K1's claim counters (`work`, nwork words) on the way: one launch per chunk, exact
 // (float32 -> float64 and the 0 / 1 contacts).  Block (x, y): samples of row y.
 __global__ void __launch_bounds__(256) k0_widen(const unsigned char* __restrict__ wire, int64_t n, int nq, int nd,
@@ -2155,7 +2158,15 @@ k1s_row_list(const int* __restrict__ rcount, const int* __restrict__ rseg, int n
   const int b = (int)blockIdx.x, t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
   auto wave_incl = [&](int v) { return k1s_wave_incl(v, lane); };
   int pre = 0;
-  for (int x = t; x < b; x += 256) pre += rseg[x];
+  if (rseg != nullptr) {
+    for (int x = t; x < b; x += 256) pre += rseg[x];
+  } else {  // short chunks: the earlier (whole) segments' counts summed here, no k1s_seg_sums launch
+    const int4* r4 = reinterpret_cast<const int4*>(rcount);
+    for (int x = t; x < (b << (K1_SEG_LOG - 2)); x += 256) {
+      const int4 v = r4[x];
+      pre += (v.x + v.y) + (v.z + v.w);
+    }
+  }
   pre = __shfl(wave_incl(pre), 63, 64);
   if (lane == 0) wsum[w] = pre;
   __syncthreads();

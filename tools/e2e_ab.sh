@@ -15,10 +15,11 @@ python - "$OUT" <<'PY'
 import sys, statistics, collections, re
 rows = collections.defaultdict(list)
 for line in open(sys.argv[1]):
-    lib = line.split()[0]
+    f = line.split()
+    lib = f[0] if len(f) < 5 or f[4] == "gram_only" else f[0] + ":" + f[4]  # per library and output mode
     m = re.search(r"best ([0-9.]+) ms\s+median ([0-9.]+) ms", line)
     rows[lib].append((float(m.group(1)), float(m.group(2))))
 for lib, v in rows.items():
-    print("%-12s n=%d  best-of-best %.3f  median-of-best %.3f  median-of-median %.3f" % (
+    print("%-18s n=%d  best-of-best %.3f  median-of-best %.3f  median-of-median %.3f" % (
         lib, len(v), min(b for b, _ in v), statistics.median(b for b, _ in v), statistics.median(m for _, m in v)))
 PY
