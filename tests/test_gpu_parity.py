@@ -381,6 +381,25 @@ def test_host_gram_only_staged_chunks(robot, N, chunks, ws_chunk):
     assert only["num_rows"] == N * model.nv
 
 
+@pytest.mark.parametrize("flags", [EMIT_GRAM, EMIT_ALL])
+def test_host_calls_restage_fresh_inputs(flags):
+    """The host entry point reuses its page-locked staging block from call to call, and K0W reads the first chunk
+    from it directly over PCIe: alternating calls on two different input sets of the same size (same chunk bounds,
+    same staging offsets) must each give their own outputs, bitwise equal to a fresh engine's — a stale first
+    chunk (cached or not yet rewritten) would return the other set's rows."""
+    model = load_robot("spot")
+    N = 20000
+    sets = [generate(model, N, config_index=1), generate(model, N, config_index=4)]
+    ins = [[x["q"].astype(np.float32), x["dq"], x["ddq"], x["tau"], x["contact"].astype(np.float32)] for x in sets]
+    fresh = [Engine(model).build(*a, flags) for a in ins]
+    assert not np.array_equal(fresh[0]["gram"], fresh[1]["gram"])
+    e = Engine(model)
+    for k in (0, 1, 0, 1, 1, 0):
+        out = e.build(*ins[k], flags)
+        for key in fresh[k]:
+            assert np.array_equal(np.asarray(out[key]), np.asarray(fresh[k][key])), (k, key)
+
+
 @pytest.mark.parametrize("robot,N", [("spot", 20001), ("g1_29dof", 3001), ("solo12", 7), ("spot", 1)])
 def test_float32_q_contact_entry_point_is_bitwise_the_float64_one(robot, N):
     """sysid_build_f32qc (q and contact in float32, as read_data returns them, demo/spot_identification.py:10-14)
