@@ -140,11 +140,12 @@ def cpu_model():
     return None
 
 
-def e2e_legs(eng, data, N, reps=3):
+def e2e_legs(eng, data, N, reps=10):
     """§8(d) end-to-end samples/s of the host entry point (numpy in -> numpy out, PCIe both ways):
     full outputs (stacked Y_proj, tau_proj, B_v, B_c + Gram) and Gram only (inputs in, 190 KB out).  The inputs in
     read_data's dtypes (demo/spot_identification.py:10-25): q and contact float32 as loaded, dq / ddq / tau float64
-    (filtered); the engine sends them in its wire format (sysid_build_f32qc)."""
+    (filtered); the engine sends them in its wire format (sysid_build_f32qc).  `ms` is the best of `reps` calls
+    (samples_per_s from it), `median_ms` their median."""
     import numpy as np
     from system_identification_amd.engine import EMIT_ALL, EMIT_GRAM
     ins = [data["q"].astype(np.float32), data["dq"], data["ddq"], data["tau"], data["contact"].astype(np.float32)]
@@ -152,14 +153,15 @@ def e2e_legs(eng, data, N, reps=3):
     res = {}
     for name, flags in (("full", EMIT_ALL), ("gram_only", EMIT_GRAM)):
         eng.build(*ins, flags)  # warm: device buffers grown once
-        best = None
+        ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
             out = eng.build(*ins, flags)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
+            ts.append(time.perf_counter() - t0)
+        best = min(ts)
         out_bytes = sum(v.nbytes for v in out.values() if hasattr(v, "nbytes"))
         res[name] = {"samples_per_s": round(N / best, 1), "ms": round(best * 1e3, 3),
+                     "median_ms": round(float(np.median(ts)) * 1e3, 3), "calls": reps,
                      "pcie_bytes": int(in_bytes + out_bytes),
                      "pcie_GBps": round((in_bytes + out_bytes) / best / 1e9, 2)}
     return res
