@@ -757,13 +757,15 @@ class Stager {
     const Wire w = wire_layout(e->nq, nd_, e->nc, n, in_.qsz);
     const unsigned char* hs = reinterpret_cast<const unsigned char*>(e->h_stage) + off_[c];
     const unsigned char* src = e->d_wire + off_[c];
-    if (c == 0 && SYSID_ZC_FIRST) {
+    void* mapped = nullptr;
+    if (c == 0 && SYSID_ZC_FIRST && hipHostGetDevicePointer(&mapped, e->h_stage, 0) != hipSuccess) {
+      (void)hipGetLastError();  // not mapped into this device: chunk 0 takes the DMA like the others
+      mapped = nullptr;
+    }
+    if (mapped != nullptr) {
       // chunk 0, the pipeline's fill: K0W reads the page-locked staging block over PCIe itself, so the compute
       // stream starts on it without a copy-engine -> compute hand-off
-      void* dp = nullptr;
-      if (hipHostGetDevicePointer(&dp, e->h_stage, 0) != hipSuccess)
-        return set_err(e, SYSID_E_DEVICE, "staging block not mapped");
-      src = static_cast<const unsigned char*>(dp) + off_[c];
+      src = static_cast<const unsigned char*>(mapped) + off_[c];
     } else {
       hipStream_t cs = e->copy_stream;
       if (hipMemcpyAsync(e->d_wire + off_[c], hs, (size_t)w.bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
