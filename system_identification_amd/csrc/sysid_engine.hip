@@ -1632,8 +1632,12 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
   if (want_gram) {
     // the whole (W+1)^2 buffer in ONE DMA into page-locked memory; gram / Atb / btb are split out on the host
     // after the synchronize (three copies into the caller's pageable arrays cost ~50 us of staged-copy overhead)
-    if (!e->h_gram) HIP_TRY(e, hipHostMalloc(reinterpret_cast<void**>(&e->h_gram),
-                                             (size_t)e->ncol * e->ncol * sizeof(double), hipHostMallocDefault));
+    // (errors past the first enqueue leave through fail(): the kernels may still be reading the staging block)
+    if (!e->h_gram && hipHostMalloc(reinterpret_cast<void**>(&e->h_gram), (size_t)e->ncol * e->ncol * sizeof(double),
+                                    hipHostMallocDefault) != hipSuccess) {
+      e->h_gram = nullptr;
+      return fail(set_err(e, SYSID_E_DEVICE, "page-locked Gram buffer: allocation failed"));
+    }
     if (hipMemcpyAsync(e->h_gram, e->d_gram, (size_t)e->ncol * e->ncol * sizeof(double), hipMemcpyDeviceToHost, st) !=
         hipSuccess)
       return fail(set_err(e, SYSID_E_DEVICE, "Gram copy failed"));
