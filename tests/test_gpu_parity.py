@@ -645,6 +645,22 @@ def test_gram_only_nullspace_rows(robot, N, cfg):
     assert errs["f32"] < 1e-5 and errs["bf16"] < 3e-2
 
 
+@pytest.mark.parametrize("N", [32768, 32769, 31745])
+def test_nullspace_row_list_one_and_two_launch_forms(N):
+    """k1s_row_list sums the earlier segments' row counts itself for chunks of up to K1S_ONEPASS_SEGS = 32 segments
+    of 1024 samples, and after k1s_seg_sums beyond: 32,768 samples (32 full segments, one launch), 32,769 (33
+    segments, the last holding one sample: two launches), 31,745 (ragged 32nd segment).  Each Gram from the
+    gathered nullspace rows equals the projector rows' Gram to 1e-10, bitwise repeatably."""
+    import torch
+    model = load_robot("spot")
+    e = eng("spot")
+    d = generate(model, N, config_index=4)
+    din = torch.from_numpy(channel_block(d)).cuda()
+    Gz, Gp = _gram_only(e, din, N), _gram_only(e, din, N, rows="projector")
+    assert rel(Gz, Gp) < 1e-10
+    assert np.array_equal(Gz, _gram_only(e, din, N))
+
+
 def test_gram_only_nullspace_degenerate_and_ill_conditioned():
     """The nullspace rows on the hard contact cases, host entry point with EMIT_GRAM only (the Gram-only path)
     against the numpy oracle's Gram of the reference's stacked P·A (1e-6): Spot with no / all / LOST=2 /
