@@ -643,6 +643,9 @@ struct HostInputs {
   int64_t ld;
 };
 
+#ifndef SYSID_FIRST_TENTHS  // the Gram-only first staged chunk, tenths of N (rounded up to half K1 rounds); -D for A/B
+#define SYSID_FIRST_TENTHS 3
+#endif
 #ifndef SYSID_ZC_FIRST  // 1: the first staged chunk is widened straight from the staging block (no DMA); -D for A/B
 #define SYSID_ZC_FIRST 1
 #endif
@@ -1554,7 +1557,7 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
     const int64_t R = k1_round_samples(e, gp, gram_nullspace(e, flags));
     if (R > 0 && N >= 2 * R) {
       const int64_t half = std::max<int64_t>(1, R / 2);
-      const int64_t first = std::min(std::max((3 * N / 10 + half - 1) / half * half, R), N - R);
+      const int64_t first = std::min(std::max((SYSID_FIRST_TENTHS * N / 10 + half - 1) / half * half, R), N - R);
       round_bounds = {0, first, N};
     } else {
       round_bounds = {0, (N + 1) / 2, N};
