@@ -1549,7 +1549,8 @@ int build_host(sysid_engine* e, const HostInputs& in, int64_t N, uint32_t flags,
   // chunks, which each add a K1 tail, a row list and a K2 pass to the kernel chain: profiles/r05_s4).  The first chunk
   // is ~30% of N in half K1 rounds (a round = every resident wave one step), at least one round: Spot 20k Gram-only
   // e2e, float32 q, 5 interleaved rounds of 12 calls: first chunk 4,096 / 5,120 / 6,144 / 7,168 samples, median
-  // 0.556 / 0.530 / 0.526 / 0.532 ms, best 0.530 / 0.514 / 0.499 / 0.509 (profiles/r05_s24).  The round-5 sweeps of
+  // 0.556 / 0.530 / 0.526 / 0.532 ms, best 0.530 / 0.514 / 0.499 / 0.509 (profiles/r05_s24); with the zero-copy first
+  // chunk, 4,096 / 6,144 / 8,192: median of per-run best 0.514 / 0.486 / 0.512 ms (profiles/r06_s24).  The round-5 sweeps of
   // these bounds, of more chunks and of more copy streams ran on environment knobs that round 6 removed (git history).
   std::vector<int64_t> round_bounds;
   const bool big = (size_t)e->in_rows * N * sizeof(double) >= ((size_t)1 << 20);
