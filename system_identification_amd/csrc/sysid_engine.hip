@@ -776,7 +776,11 @@ class Stager {
           hipStreamWaitEvent(st, e->stage_ev[c], 0) != hipSuccess)
         return set_err(e, SYSID_E_DEVICE, "input copy failed");
     }
-    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (n + 1023) / 1024));
+#ifndef SYSID_K0W_ITERS  // samples per K0W lane and row (grid-stride iterations); -D for A/B
+#define SYSID_K0W_ITERS 4
+#endif
+    const int64_t per_block = 256 * SYSID_K0W_ITERS;
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(65536 / per_block, (n + per_block - 1) / per_block));
     hipLaunchKernelGGL(k0_widen, dim3(gx, (unsigned)(e->nq + nd_ + e->nc)), dim3(256), 0, st, src, n, e->nq, nd_,
                        in_.qsz, w.d, w.c, e->d_in + c0, N_, work, (int)(WORK_BYTES / 8));
     HIP_TRY(e, hipGetLastError());
